@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X IB-LBM hot path: BASELINE.json metric
+"MLUPS and achieved-HBM-GB/s, 4096^2 D2Q9 channel, 1/2/4/8 MI355X".
+
+One step = one reference iteration (main.cu:852-909) over the whole 4096 x 4096 channel
+(periodic x, bounce-back / mirror walls, TRT + Guo forcing, uniform body force, no IB):
+one fused pull-stream + collide launch per slab.  N > 1: x-slab decomposition of the SAME
+4096^2 lattice (strong scaling), one process per GPU, one-column halo via RCCL.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f64|f32] [--nx 4096 --ny 4096]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+         --master-port P bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes of the collide-stream
+kernel (18 populations x 8 B = 144 B per cell in f64) x cells per launch / mean launch time
+measured with HIP events on the stream the kernel runs on; `roofline.traffic` = HBM bytes
+per launch from rocprofv3 PMC counters (profiles/pmc_traffic.json, FETCH_SIZE doubled per
+MI355X_MICROARCH.md §HBM) when a matching profile exists.  `cpu_baseline` = the oracle
+(reference kernels restated in C, unfused AoS sequence) on the host cores, rank 0 at N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "MLUPS and achieved-HBM-GB/s, 4096² D2Q9 channel, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=500)
+    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--nx", type=int, default=4096)
+    p.add_argument("--ny", type=int, default=4096)
+    p.add_argument("--precision", choices=["f64", "f32"], default="f64")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU sample duration")
+    p.add_argument("--no-profile-events", action="store_true", help="skip per-launch HIP events")
+    return p.parse_args()
+
+
+def cpu_baseline(nx, ny, budget_s):
+    """The reference's own unfused sequence (equilibrium, collision, streaming, macro, spread's
+    u correction; AoS fp64) restated in C (oracle/), OpenMP over the host cores, timed on a
+    bounded number of steps of the same workload."""
+    from oracle import oracle as O
+    from cuda_iblb_11_amd import workloads as W
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    kind = "port"
+    try:
+        O.build(native=True)
+        O.load(native=True)
+        native = True
+    except Exception:
+        O.load()
+        native = False
+    O.set_threads(threads)
+    rho, u = W.perturbed_state(nx, ny, W.SEED)
+    sim = O.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=W.BODY_FORCE)
+    del rho, u
+    t0 = time.perf_counter()
+    sim.step(1)  # warm-up + size the sample
+    one = time.perf_counter() - t0
+    n = int(max(1, min(50, budget_s / max(one, 1e-6))))
+    t0 = time.perf_counter()
+    sim.step(n)
+    dt = time.perf_counter() - t0
+    mlups = nx * ny * n / dt / 1e6
+    return {"value": round(mlups, 3), "unit": "MLUPS", "cores": threads, "kind": kind,
+            "sample": f"{n} steps of the {nx}x{ny} f64 channel, reference unfused AoS sequence restated in C "
+                      f"(oracle/oracle.c, {'-march=native' if native else 'x86-64-v2'}, OpenMP {threads} threads), "
+                      f"{dt:.1f} s"}
+
+
+def pmc_traffic(workload_key):
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except Exception:
+        return None, None
+    e = d.get(workload_key)
+    if not e:
+        return None, None
+    return e.get("hbm_bytes_per_launch"), e.get("source")
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+
+    import cuda_iblb_11_amd as P
+    from cuda_iblb_11_amd import workloads as W
+
+    nx, ny = a.nx, a.ny
+    xb, xc = P.plan_slabs(nx, world)[rank]
+    lat = P.Lattice(nx, ny, W.TAU, W.TAU2, precision=a.precision, body_force=W.BODY_FORCE, device=local,
+                    x_begin=xb, x_count=xc if world > 1 else 0)
+    rho, u = W.perturbed_state(nx, ny, W.SEED)
+    lat.set_state(P.split_state(rho, 1, nx, ny, xb, xc), P.split_state(u, 2, nx, ny, xb, xc))
+    del rho, u
+    if distributed:
+        uid = [P.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        lat.attach_rccl(uid[0], world, rank)
+
+    lat.step(a.warmup)
+    lat.synchronize()
+    lat.set_profiling(not a.no_profile_events)
+    lat.timing(reset=True)
+
+    def barrier():
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    lat.step(a.steps)
+    lat.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    tm = lat.timing(reset=True)
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        fl = torch.tensor([tm["fused_ms"] / max(tm["fused_launches"], 1)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(fl, op=dist.ReduceOp.MAX)
+        launch_ms = float(fl.item())
+    else:
+        launch_ms = tm["fused_ms"] / max(tm["fused_launches"], 1)
+
+    # sanity: the state must stay finite (macro() is collective for an RCCL group)
+    rho_s, _ = lat.macro()
+    finite = bool(np.isfinite(rho_s).all())
+    if distributed:
+        fin = torch.tensor([1.0 if finite else 0.0], device="cuda")
+        dist.all_reduce(fin, op=dist.ReduceOp.MIN)
+        finite = bool(fin.item() > 0)
+
+    cells = nx * ny
+    mlups = cells * a.steps / elapsed / 1e6
+    bytes_per_cell = 18 * (8 if a.precision == "f64" else 4)
+    cells_per_launch = xc * ny
+    achieved = bytes_per_cell * cells_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else None
+    key = f"{a.precision}_{nx}x{ny}_n{world}"
+    traffic, traffic_src = pmc_traffic(key)
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            lat.close()
+            cpu = cpu_baseline(nx, ny, a.cpu_seconds)
+        out = {
+            "metric": METRIC,
+            "value": round(mlups, 2),
+            "unit": "MLUPS",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": a.precision,
+            "data": "synthetic (rho = 1 + 1e-3 xi, u = 1e-3 xi, numpy seed 12345; body force 1e-6)",
+            "config": {
+                "workload": f"M: {nx}x{ny} D2Q9 channel (periodic x, bounce-back y=0, mirror y=Y-1), "
+                            f"TRT+Guo, reference TAU/TAU2, no IB; one fused pull-stream+collide launch per step",
+                "nx": nx, "ny": ny, "global_cells": cells,
+                "parallelism": f"x-slab x{world}" + (" (RCCL halo)" if world > 1 else ""),
+            },
+            "achieved_hbm_gbps": round(mlups * 1e6 * bytes_per_cell / 1e9, 1),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": None if achieved is None else round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic,
+                "kernel": "fused_kernel (lbm_kernels.hip)",
+                "bytes_per_cell": bytes_per_cell,
+                "cells_per_launch": cells_per_launch,
+                "launch_ms": round(launch_ms, 5),
+                "traffic_source": traffic_src,
+            },
+            "cpu_baseline": cpu,
+            "state_finite": finite,
+        }
+        print(json.dumps(out), flush=True)
+    lat.close()
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,923 @@
+// iblb_ctx.hip — the fused context API of include/iblb.h: state, time stepping, slab
+// decomposition (local and RCCL transports), readers in the reference layouts.
+//
+// Time-step bookkeeping.  The reference iteration (main.cu:852-909) is
+//   f0,F = equilibrium(u^t, rho^t, force^t); f1 = collision(f^t); f^{t+1} = stream(f1);
+//   rho^{t+1}, u_raw = macro(f^{t+1}); F_s = interpolate(...); force^{t+1}, u^{t+1} = spread(...)
+// The context stores g = f1^{t-1} (post-collision, not yet streamed).  One fused launch
+// pulls f^t from g, recomputes rho^t and u^t = (sum c f + force^t/2)/rho^t, collides and
+// stores f1^t.  force^t (the IB part of the PREVIOUS reference iteration) is computed
+// lazily just before it is needed — before the next collide, before a reader, or before
+// the Lagrangian points change — so every call sees exactly the reference's state.
+// The flux term q(u^t) the reference adds at the end of iteration t-1 is added by the
+// collide of step t; iblb_get_flux() adds the not-yet-collided last term on demand.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/iblb.h"
+#include "iblb_kernels.h"
+
+using namespace iblb;
+
+namespace {
+
+enum Phase { PH_EMPTY = 0, PH_BOOT = 1, PH_RUN = 2 };
+enum IbState { IB_NONE = 0, IB_PENDING = 1, IB_READY = 2 };
+enum Transport { TR_NONE = 0, TR_LOCAL = 1, TR_RCCL = 2 };
+
+constexpr long GUARD = 512;  // elements in front of / behind every population buffer
+
+std::string g_create_error;
+
+long env_long(const char* name, long dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::strtol(v, nullptr, 10) : dflt;
+}
+
+}  // namespace
+
+struct iblb_ctx {
+    iblb_config cfg{};
+    int nx = 0, ny = 0, x_begin = 0, ncol = 0;
+    int prec = IBLB_PREC_F64;
+    size_t esize = 8;
+    int V = 2, nch = 1;
+    Layout L{};
+    long fplane = 0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Coef coef{};
+    // populations: two buffers, `cur` holds the state
+    char* g_alloc[2] = {nullptr, nullptr};
+    void* g[2] = {nullptr, nullptr};
+    int cur = 0;
+    // halo exchange buffers (multi-slab): 3 slots of `col` elements each, guarded
+    char* halo_alloc = nullptr;
+    void* recv_left = nullptr;
+    void* recv_right = nullptr;
+    void* send_left = nullptr;
+    void* send_right = nullptr;
+    // boot arrays (slab layout)
+    double* rho0 = nullptr;
+    double* u0 = nullptr;
+    double* force0 = nullptr;
+    // immersed boundary
+    int max_points = 0, ns = 0;
+    float* d_s = nullptr;
+    float* d_us = nullptr;
+    float* d_Fs = nullptr;
+    int* d_eps = nullptr;
+    double* d_nv = nullptr;
+    double* d_nv_tmp = nullptr;
+    double* fdense = nullptr;
+    uint8_t* flags = nullptr;
+    // flux: d_Q[0] cumulative, d_Q[1] scratch
+    double* d_Q = nullptr;
+    // state machine
+    int phase = PH_EMPTY;
+    long long t = 0;
+    int ib_state = IB_NONE;
+    bool halo_valid = false;
+    // transport
+    int transport = TR_NONE;
+    iblb_ctx* left = nullptr;
+    iblb_ctx* right = nullptr;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    double fused_ms = 0., ib_ms = 0., halo_ms = 0.;
+    long long fused_launches = 0;
+    std::vector<std::pair<int, size_t>> ev_kind;  // (kind, pair index)
+    std::string err;
+};
+
+namespace {
+
+int fail(iblb_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    else g_create_error = msg;
+    return code;
+}
+
+int hip_fail(iblb_ctx* c, hipError_t e, const char* what) {
+    return fail(c, e == hipErrorOutOfMemory ? IBLB_ERR_NOMEM : IBLB_ERR_HIP,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(c, expr)                                               \
+    do {                                                               \
+        hipError_t e_ = (expr);                                        \
+        if (e_ != hipSuccess) return hip_fail((c), e_, #expr);         \
+    } while (0)
+
+#define NCCL_TRY(c, expr)                                                                           \
+    do {                                                                                            \
+        ncclResult_t r_ = (expr);                                                                   \
+        if (r_ != ncclSuccess) return fail((c), IBLB_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+template <typename T>
+T* gptr(iblb_ctx* c, int which) { return (T*)c->g[which]; }
+
+bool single_slab(const iblb_ctx* c) { return c->ncol == c->nx && c->transport != TR_LOCAL && c->nranks <= 1; }
+bool ib_active(const iblb_ctx* c) { return c->max_points > 0 && c->ns > 0; }
+
+template <typename T>
+Halo<T> halo_of(iblb_ctx* c, int which) {
+    Halo<T> H;
+    const Layout& L = c->L;
+    if (single_slab(c)) {
+        const T* g = gptr<T>(c, which);
+        for (int p = 0; p < 3; ++p) {
+            H.left[p] = g + left_plane(p) * L.plane + (long)(L.ncol - 1) * L.col;
+            H.right[p] = g + right_plane(p) * L.plane;
+        }
+    } else {
+        for (int p = 0; p < 3; ++p) {
+            H.left[p] = (const T*)c->recv_left + p * L.col;
+            H.right[p] = (const T*)c->recv_right + p * L.col;
+        }
+    }
+    return H;
+}
+
+template <typename T>
+void send_ptrs(iblb_ctx* c, T* sl[3], T* sr[3]) {
+    for (int p = 0; p < 3; ++p) {
+        sl[p] = single_slab(c) ? nullptr : (T*)c->send_left + p * c->L.col;
+        sr[p] = single_slab(c) ? nullptr : (T*)c->send_right + p * c->L.col;
+    }
+}
+
+// ---- profiling --------------------------------------------------------------------------
+enum EvKind { EV_FUSED = 0, EV_IB = 1, EV_HALO = 2 };
+
+int ev_begin(iblb_ctx* c, size_t* idx) {
+    if (!c->prof) return IBLB_OK;
+    if (c->ev_used + 2 > c->ev_pool.size()) {
+        for (int k = 0; k < 64; ++k) {
+            hipEvent_t e;
+            HIP_TRY(c, hipEventCreate(&e));
+            c->ev_pool.push_back(e);
+        }
+    }
+    *idx = c->ev_used;
+    c->ev_used += 2;
+    HIP_TRY(c, hipEventRecord(c->ev_pool[*idx], c->stream));
+    return IBLB_OK;
+}
+
+int ev_end(iblb_ctx* c, size_t idx, int kind) {
+    if (!c->prof) return IBLB_OK;
+    HIP_TRY(c, hipEventRecord(c->ev_pool[idx + 1], c->stream));
+    c->ev_kind.push_back({kind, idx});
+    if (c->ev_used >= 8192) {  // bound the pool: drain what is recorded
+        HIP_TRY(c, hipEventSynchronize(c->ev_pool[idx + 1]));
+        for (auto& kv : c->ev_kind) {
+            float ms = 0.f;
+            HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_pool[kv.second], c->ev_pool[kv.second + 1]));
+            if (kv.first == EV_FUSED) { c->fused_ms += ms; c->fused_launches++; }
+            else if (kv.first == EV_IB) c->ib_ms += ms;
+            else c->halo_ms += ms;
+        }
+        c->ev_kind.clear();
+        c->ev_used = 0;
+    }
+    return IBLB_OK;
+}
+
+// ---- halo exchange ----------------------------------------------------------------------
+int exchange_rccl(iblb_ctx* c) {
+    size_t ev = 0;
+    int rc = ev_begin(c, &ev);
+    if (rc) return rc;
+    const size_t n = 3 * (size_t)c->L.col;
+    const ncclDataType_t dt = c->prec == IBLB_PREC_F64 ? ncclFloat64 : ncclFloat32;
+    const int lr = (c->rank + c->nranks - 1) % c->nranks, rr = (c->rank + 1) % c->nranks;
+    NCCL_TRY(c, ncclGroupStart());
+    NCCL_TRY(c, ncclSend(c->send_right, n, dt, rr, c->comm, c->stream));
+    NCCL_TRY(c, ncclSend(c->send_left, n, dt, lr, c->comm, c->stream));
+    NCCL_TRY(c, ncclRecv(c->recv_left, n, dt, lr, c->comm, c->stream));
+    NCCL_TRY(c, ncclRecv(c->recv_right, n, dt, rr, c->comm, c->stream));
+    NCCL_TRY(c, ncclGroupEnd());
+    c->halo_valid = true;
+    return ev_end(c, ev, EV_HALO);
+}
+
+int exchange_local(iblb_ctx* c) {
+    const size_t bytes = 3 * (size_t)c->L.col * c->esize;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMemcpyAsync(c->recv_left, c->left->send_right, bytes, hipMemcpyDefault, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->recv_right, c->right->send_left, bytes, hipMemcpyDefault, c->stream));
+    c->halo_valid = true;
+    return IBLB_OK;
+}
+
+// ---- immersed boundary ------------------------------------------------------------------
+template <typename T>
+int ib_nodes(iblb_ctx* c) {
+    HIP_TRY(c, launch_ib_nodes<T>(gptr<T>(c, c->cur), c->L, halo_of<T>(c, c->cur), c->nx, c->x_begin, c->ns, c->d_s,
+                                  c->d_nv, c->stream));
+    return IBLB_OK;
+}
+
+int ib_nodes_any(iblb_ctx* c) { return c->prec == IBLB_PREC_F64 ? ib_nodes<double>(c) : ib_nodes<float>(c); }
+
+int ib_finish(iblb_ctx* c) {
+    const int rpc = 64 * c->V;
+    HIP_TRY(c, hipMemsetAsync(c->flags, 0, (size_t)c->ncol * c->nch, c->stream));
+    HIP_TRY(c, launch_ib_interp(c->nx, c->ny, c->ns, c->d_s, c->d_us, c->d_nv, c->d_Fs, c->stream));
+    HIP_TRY(c, launch_ib_spread(c->L, c->nx, c->x_begin, c->ns, c->d_s, c->d_Fs, c->d_eps, c->fdense, c->fplane,
+                                c->flags, c->nch, rpc, c->stream));
+    c->ib_state = IB_READY;
+    return IBLB_OK;
+}
+
+// force^t for a context that is alone or in an RCCL group (local groups: group code)
+int ensure_halo(iblb_ctx* c) {
+    if (c->halo_valid || single_slab(c)) return IBLB_OK;
+    if (c->transport == TR_RCCL) return exchange_rccl(c);
+    return fail(c, IBLB_ERR_STATE, "slab halo not available: link the slabs (iblb_link_local / iblb_attach_rccl)");
+}
+
+int ensure_force(iblb_ctx* c) {
+    if (c->ib_state != IB_PENDING) return IBLB_OK;
+    if (c->transport == TR_LOCAL)
+        return fail(c, IBLB_ERR_STATE, "local group: advance with iblb_group_step");
+    int rc = ensure_halo(c);
+    if (rc) return rc;
+    size_t ev = 0;
+    if ((rc = ev_begin(c, &ev))) return rc;
+    if ((rc = ib_nodes_any(c))) return rc;
+    if (c->transport == TR_RCCL && c->nranks > 1)
+        NCCL_TRY(c, ncclAllReduce(c->d_nv, c->d_nv, 27 * (size_t)c->ns, ncclFloat64, ncclSum, c->comm, c->stream));
+    if ((rc = ib_finish(c))) return rc;
+    return ev_end(c, ev, EV_IB);
+}
+
+// ---- the step -----------------------------------------------------------------------------
+template <typename T>
+int launch_boot_step(iblb_ctx* c) {
+    T* sl[3];
+    T* sr[3];
+    send_ptrs<T>(c, sl, sr);
+    HIP_TRY(c, launch_boot<T>(gptr<T>(c, c->cur), gptr<T>(c, 1 - c->cur), c->L, c->rho0, c->u0, c->force0, c->fplane,
+                              sl, sr, c->coef, c->stream));
+    return IBLB_OK;
+}
+
+template <typename T>
+int launch_fused_step(iblb_ctx* c, int col_begin, int ncols) {
+    FusedArgs<T> a;
+    a.src = gptr<T>(c, c->cur);
+    a.dst = gptr<T>(c, 1 - c->cur);
+    a.L = c->L;
+    a.H = halo_of<T>(c, c->cur);
+    send_ptrs<T>(c, a.send_left, a.send_right);
+    a.col_begin = col_begin;
+    a.ncols = ncols;
+    a.nch = c->nch;
+    const bool ib = c->ib_state == IB_READY;
+    a.flags = ib ? c->flags : nullptr;
+    a.fdense = c->fdense;
+    a.fplane = c->fplane;
+    const int fc = c->cfg.flux_column - c->x_begin;
+    a.flux_col = (fc >= 0 && fc < c->ncol) ? fc : -1;
+    a.flux_norm = c->cfg.flux_norm;
+    a.Q = c->d_Q;
+    a.c = c->coef;
+    size_t ev = 0;
+    int rc = ev_begin(c, &ev);
+    if (rc) return rc;
+    HIP_TRY(c, launch_fused<T>(a, c->stream));
+    return ev_end(c, ev, EV_FUSED);
+}
+
+int free_boot(iblb_ctx* c) {
+    if (c->rho0) (void)hipFree(c->rho0);
+    if (c->u0) (void)hipFree(c->u0);
+    if (c->force0) (void)hipFree(c->force0);
+    c->rho0 = c->u0 = c->force0 = nullptr;
+    return IBLB_OK;
+}
+
+// One reference iteration for a context whose halo (if any) and force^t are in place.
+int advance(iblb_ctx* c) {
+    int rc;
+    const bool f64 = c->prec == IBLB_PREC_F64;
+    if (c->phase == PH_BOOT) {
+        rc = f64 ? launch_boot_step<double>(c) : launch_boot_step<float>(c);
+        if (rc) return rc;
+        c->phase = PH_RUN;
+    } else {
+        rc = f64 ? launch_fused_step<double>(c, 0, c->ncol) : launch_fused_step<float>(c, 0, c->ncol);
+        if (rc) return rc;
+    }
+    c->cur = 1 - c->cur;
+    c->t++;
+    c->halo_valid = false;
+    c->ib_state = ib_active(c) ? IB_PENDING : IB_NONE;
+    return IBLB_OK;
+}
+
+int check_ready(iblb_ctx* c) {
+    if (c->phase == PH_EMPTY) return fail(c, IBLB_ERR_STATE, "no state: call iblb_set_state first");
+    if (!single_slab(c) && c->transport == TR_NONE)
+        return fail(c, IBLB_ERR_STATE, "slab context is not linked to its neighbours");
+    return IBLB_OK;
+}
+
+int step_one(iblb_ctx* c) {
+    int rc;
+    if (c->phase == PH_RUN) {
+        if ((rc = ensure_halo(c))) return rc;
+        if ((rc = ensure_force(c))) return rc;
+    }
+    rc = advance(c);
+    if (rc) return rc;
+    if (c->phase == PH_RUN && c->t == 1 && c->rho0) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        free_boot(c);
+    }
+    return IBLB_OK;
+}
+
+size_t round_up(size_t v, size_t m) { return (v + m - 1) / m * m; }
+
+// Allocation zeroed on the context's (non-blocking) stream, so later work on that stream is
+// ordered after the clear.
+int alloc_zero(iblb_ctx* c, void** p, size_t bytes) {
+    HIP_TRY(c, hipMalloc(p, bytes));
+    HIP_TRY(c, hipMemsetAsync(*p, 0, bytes, c->stream));
+    return IBLB_OK;
+}
+
+// Scratch device buffer freed at scope exit.
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+// Make halos and force^t of the current state available to a reader.
+int prepare_read(iblb_ctx* c) {
+    int rc = check_ready(c);
+    if (rc) return rc;
+    if (c->phase != PH_RUN) return IBLB_OK;
+    if (c->transport == TR_LOCAL) {
+        if (!c->halo_valid || c->ib_state == IB_PENDING)
+            return fail(c, IBLB_ERR_STATE, "local group state not prepared (use iblb_group_step)");
+        return IBLB_OK;
+    }
+    if ((rc = ensure_halo(c))) return rc;
+    return ensure_force(c);
+}
+
+}  // namespace
+
+// ============================================================================================
+extern "C" {
+
+const char* iblb_version(void) { return "iblb-mi355x 0.1 (gfx950)"; }
+
+int iblb_device_count(int* n) {
+    if (!n) return IBLB_ERR_ARG;
+    int k = 0;
+    if (hipGetDeviceCount(&k) != hipSuccess) k = 0;
+    *n = k;
+    return IBLB_OK;
+}
+
+int iblb_config_default(iblb_config* cfg) {
+    if (!cfg) return IBLB_ERR_ARG;
+    std::memset(cfg, 0, sizeof(*cfg));
+    // main.cu:267-321 with the default arguments c_num=6, c_space=48, Re=1, T=1e5
+    cfg->nx = 288;
+    cfg->ny = 192;
+    const double SPEED = 0.8 * 1000 / 100000.;
+    const double cs = 0.577;  // main.cu:27
+    cfg->tau = (SPEED * 96) / (1.0 * cs * cs) + 1. / 2.;
+    cfg->tau2 = 1. / (12. * (cfg->tau - (1. / 2.))) + (1. / 2.);
+    cfg->precision = IBLB_PREC_F64;
+    cfg->flux_norm = 192.;
+    cfg->flux_column = cfg->nx - 5;
+    cfg->device = 0;
+    cfg->x_begin = 0;
+    cfg->x_count = 0;
+    cfg->max_points = 0;
+    return IBLB_OK;
+}
+
+const char* iblb_last_error(const iblb_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
+    if (!cfg || !out) return fail(nullptr, IBLB_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (cfg->nx < 1 || cfg->ny < 2) return fail(nullptr, IBLB_ERR_ARG, "need nx >= 1 and ny >= 2");
+    if (!(cfg->tau > 0.5) || !(cfg->tau2 > 0.5)) return fail(nullptr, IBLB_ERR_ARG, "need tau, tau2 > 0.5");
+    if (cfg->precision != IBLB_PREC_F64 && cfg->precision != IBLB_PREC_F32)
+        return fail(nullptr, IBLB_ERR_ARG, "precision must be IBLB_PREC_F64 or IBLB_PREC_F32");
+    if (cfg->flux_norm == 0.) return fail(nullptr, IBLB_ERR_ARG, "flux_norm must be non-zero");
+    const int xb = cfg->x_count > 0 ? cfg->x_begin : 0;
+    const int nc = cfg->x_count > 0 ? cfg->x_count : cfg->nx;
+    if (xb < 0 || xb + nc > cfg->nx) return fail(nullptr, IBLB_ERR_ARG, "slab outside the lattice");
+    if (cfg->max_points < 0) return fail(nullptr, IBLB_ERR_ARG, "max_points < 0");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(nullptr, IBLB_ERR_NODEVICE, "no HIP device visible (the HIP path has no CPU fallback)");
+    if (cfg->device < 0 || cfg->device >= ndev) return fail(nullptr, IBLB_ERR_ARG, "device ordinal out of range");
+
+    iblb_ctx* c = new iblb_ctx();
+    c->cfg = *cfg;
+    c->nx = cfg->nx;
+    c->ny = cfg->ny;
+    c->x_begin = xb;
+    c->ncol = nc;
+    c->prec = cfg->precision;
+    c->esize = c->prec == IBLB_PREC_F64 ? 8 : 4;
+    c->V = c->prec == IBLB_PREC_F64 ? vec_of<double>() : vec_of<float>();
+    c->nch = chunks_per_column(c->ny, c->V);
+    c->device = cfg->device;
+    c->max_points = cfg->max_points;
+    if (c->cfg.flux_column < 0) c->cfg.flux_column = c->nx - 5;
+
+    const double tau = cfg->tau, tau2 = cfg->tau2, cs = 0.57735;
+    c->coef.omega_p = 1. / tau;
+    c->coef.omega_m = 1. / tau2;
+    c->coef.kguo = 1. - 1. / (2. * tau);
+    c->coef.inv_cs2 = 1. / (cs * cs);
+    c->coef.inv_cs4 = 1. / (cs * cs * cs * cs);
+    c->coef.inv_2cs2 = 1. / (2 * cs * cs);
+    c->coef.inv_2cs4 = 1. / (2 * cs * cs * cs * cs);
+    c->coef.gx = cfg->body_force[0];
+    c->coef.gy = cfg->body_force[1];
+
+    auto bail = [&](int rc) { g_create_error = c->err; iblb_destroy(c); return rc; };
+    if (hipSetDevice(c->device) != hipSuccess) return bail(fail(c, IBLB_ERR_HIP, "hipSetDevice failed"));
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(c, IBLB_ERR_HIP, "hipStreamCreate failed"));
+
+    // slab layout: column stride a multiple of one wave's rows, planes padded apart
+    const long col = (long)round_up((size_t)c->ny, (size_t)(64 * c->V));
+    const long pad = env_long("IBLB_PLANE_PAD", 64 * c->V);
+    c->L.ny = c->ny;
+    c->L.ncol = c->ncol;
+    c->L.col = col;
+    c->L.plane = (long)c->ncol * col + pad;
+    c->fplane = (long)c->ncol * col;
+    const size_t gbytes = (size_t)(9 * c->L.plane + 2 * GUARD) * c->esize;
+    for (int b = 0; b < 2; ++b) {
+        int rc = alloc_zero(c, (void**)&c->g_alloc[b], gbytes);
+        if (rc) return bail(rc);
+        c->g[b] = c->g_alloc[b] + GUARD * c->esize;
+    }
+    // halo buffers: recv_left, recv_right, send_left, send_right; each 3 slots + guards
+    {
+        const size_t slot = (size_t)(3 * col + 2 * GUARD) * c->esize;
+        int rc = alloc_zero(c, (void**)&c->halo_alloc, 4 * slot);
+        if (rc) return bail(rc);
+        c->recv_left = c->halo_alloc + 0 * slot + GUARD * c->esize;
+        c->recv_right = c->halo_alloc + 1 * slot + GUARD * c->esize;
+        c->send_left = c->halo_alloc + 2 * slot + GUARD * c->esize;
+        c->send_right = c->halo_alloc + 3 * slot + GUARD * c->esize;
+    }
+    int rc = alloc_zero(c, (void**)&c->d_Q, 4 * sizeof(double));
+    if (rc) return bail(rc);
+    if (c->max_points > 0) {
+        const size_t np = (size_t)c->max_points;
+        if ((rc = alloc_zero(c, (void**)&c->d_s, 2 * np * sizeof(float)))) return bail(rc);
+        if ((rc = alloc_zero(c, (void**)&c->d_us, 2 * np * sizeof(float)))) return bail(rc);
+        if ((rc = alloc_zero(c, (void**)&c->d_Fs, 2 * np * sizeof(float)))) return bail(rc);
+        if ((rc = alloc_zero(c, (void**)&c->d_eps, np * sizeof(int)))) return bail(rc);
+        if ((rc = alloc_zero(c, (void**)&c->d_nv, 27 * np * sizeof(double)))) return bail(rc);
+        if ((rc = alloc_zero(c, (void**)&c->d_nv_tmp, 27 * np * sizeof(double)))) return bail(rc);
+        if ((rc = alloc_zero(c, (void**)&c->fdense, 2 * (size_t)c->fplane * sizeof(double)))) return bail(rc);
+        if ((rc = alloc_zero(c, (void**)&c->flags, (size_t)c->ncol * c->nch))) return bail(rc);
+    }
+    *out = c;
+    return IBLB_OK;
+}
+
+void iblb_destroy(iblb_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    for (int b = 0; b < 2; ++b)
+        if (c->g_alloc[b]) (void)hipFree(c->g_alloc[b]);
+    void* bufs[] = {c->halo_alloc, c->rho0, c->u0, c->force0, c->d_s, c->d_us, c->d_Fs,
+                    c->d_eps, c->d_nv, c->d_nv_tmp, c->fdense, c->flags, c->d_Q};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->left && c->left->right == c) c->left->right = nullptr;
+    if (c->right && c->right->left == c) c->right->left = nullptr;
+    delete c;
+}
+
+int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double* f, const double* force) {
+    if (!c) return IBLB_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const long N = (long)c->ncol * c->ny;
+    const size_t nb = (size_t)N * sizeof(double);
+    free_boot(c);
+    int rc;
+    if ((rc = alloc_zero(c, (void**)&c->rho0, (size_t)c->fplane * sizeof(double)))) return rc;
+    if ((rc = alloc_zero(c, (void**)&c->u0, 2 * (size_t)c->fplane * sizeof(double)))) return rc;
+    if ((rc = alloc_zero(c, (void**)&c->force0, 2 * (size_t)c->fplane * sizeof(double)))) return rc;
+
+    DevBuf d_rho, d_u, d_force, d_f, d_F;
+    HIP_TRY(c, hipMalloc(&d_rho.p, nb));
+    HIP_TRY(c, hipMalloc(&d_u.p, 2 * nb));
+    HIP_TRY(c, hipMalloc(&d_force.p, 2 * nb));
+    if (rho) {
+        HIP_TRY(c, hipMemcpy(d_rho.p, rho, nb, hipMemcpyHostToDevice));
+    } else {
+        std::vector<double> ones((size_t)N, 1.0);  // RHO_0 (main.cu:28, 638)
+        HIP_TRY(c, hipMemcpy(d_rho.p, ones.data(), nb, hipMemcpyHostToDevice));
+    }
+    if (u) HIP_TRY(c, hipMemcpy(d_u.p, u, 2 * nb, hipMemcpyHostToDevice));
+    else HIP_TRY(c, hipMemsetAsync(d_u.p, 0, 2 * nb, c->stream));
+    if (force) HIP_TRY(c, hipMemcpy(d_force.p, force, 2 * nb, hipMemcpyHostToDevice));
+    else HIP_TRY(c, hipMemsetAsync(d_force.p, 0, 2 * nb, c->stream));
+    HIP_TRY(c, hipMalloc(&d_f.p, 9 * nb));
+    if (f) {
+        HIP_TRY(c, hipMemcpy(d_f.p, f, 9 * nb, hipMemcpyHostToDevice));
+    } else {
+        // main.cu:720-754: f = f0 = equilibrium(u, rho) with force 0
+        DevBuf zero;
+        HIP_TRY(c, hipMalloc(&d_F.p, 9 * nb));
+        HIP_TRY(c, hipMalloc(&zero.p, 2 * nb));
+        HIP_TRY(c, hipMemsetAsync(zero.p, 0, 2 * nb, c->stream));
+        rc = iblb_equilibrium((const double*)d_u.p, (const double*)d_rho.p, (double*)d_f.p, (const double*)zero.p,
+                              (double*)d_F.p, c->ncol, c->ny, c->cfg.tau, c->stream);
+        if (rc) return fail(c, rc, "initial equilibrium launch failed");
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    if (c->prec == IBLB_PREC_F64)
+        HIP_TRY(c, launch_pop_in<double>((const double*)d_f.p, gptr<double>(c, c->cur), c->L, c->stream));
+    else
+        HIP_TRY(c, launch_pop_in<float>((const double*)d_f.p, gptr<float>(c, c->cur), c->L, c->stream));
+    HIP_TRY(c, launch_field_in((const double*)d_rho.p, c->rho0, c->L, 1, c->fplane, c->stream));
+    HIP_TRY(c, launch_field_in((const double*)d_u.p, c->u0, c->L, 2, c->fplane, c->stream));
+    HIP_TRY(c, launch_field_in((const double*)d_force.p, c->force0, c->L, 2, c->fplane, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_Q, 0, 4 * sizeof(double), c->stream));
+    if (c->fdense) {
+        HIP_TRY(c, hipMemsetAsync(c->fdense, 0, 2 * (size_t)c->fplane * sizeof(double), c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->flags, 0, (size_t)c->ncol * c->nch, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->phase = PH_BOOT;
+    c->t = 0;
+    c->ib_state = IB_NONE;
+    c->halo_valid = false;
+    return IBLB_OK;
+}
+
+int iblb_set_lagrangian(iblb_ctx* c, int ns, const float* s, const float* u_s, const int* epsilon) {
+    if (!c || ns < 0) return IBLB_ERR_ARG;
+    if (ns > c->max_points) return fail(c, IBLB_ERR_ARG, "ns exceeds max_points of the context");
+    if (ns > 0 && (!s || !u_s)) return IBLB_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    // force^t still owed to the old points: evaluate it before they change
+    if (c->ib_state == IB_PENDING) {
+        if (c->transport == TR_LOCAL)
+            return fail(c, IBLB_ERR_STATE, "local group: set points between iblb_group_step calls only");
+        int rc = ensure_force(c);
+        if (rc) return rc;
+    }
+    if (ns > 0) {
+        HIP_TRY(c, hipMemcpyAsync(c->d_s, s, 2 * (size_t)ns * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->d_us, u_s, 2 * (size_t)ns * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        if (epsilon) {
+            HIP_TRY(c, hipMemcpyAsync(c->d_eps, epsilon, (size_t)ns * sizeof(int), hipMemcpyHostToDevice, c->stream));
+        } else {
+            std::vector<int> ones((size_t)ns, 1);
+            HIP_TRY(c, hipMemcpyAsync(c->d_eps, ones.data(), (size_t)ns * sizeof(int), hipMemcpyHostToDevice, c->stream));
+        }
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    c->ns = ns;
+    return IBLB_OK;
+}
+
+int iblb_step(iblb_ctx* c, int nsteps) {
+    if (!c || nsteps < 0) return IBLB_ERR_ARG;
+    if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: use iblb_group_step");
+    int rc = check_ready(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    for (int s = 0; s < nsteps; ++s)
+        if ((rc = step_one(c))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return IBLB_OK;
+}
+
+int iblb_get_macro(iblb_ctx* c, double* rho, double* u) {
+    if (!c) return IBLB_ERR_ARG;
+    int rc = prepare_read(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const long N = (long)c->ncol * c->ny;
+    const size_t nb = (size_t)N * sizeof(double);
+    DevBuf dr, du;
+    HIP_TRY(c, hipMalloc(&dr.p, nb));
+    HIP_TRY(c, hipMalloc(&du.p, 2 * nb));
+    if (c->phase == PH_BOOT) {
+        HIP_TRY(c, launch_field_out(c->rho0, (double*)dr.p, c->L, 1, c->fplane, 0., 0., c->stream));
+        HIP_TRY(c, launch_field_out(c->u0, (double*)du.p, c->L, 2, c->fplane, 0., 0., c->stream));
+    } else {
+        const double* fd = c->ib_state == IB_READY ? c->fdense : nullptr;
+        if (c->prec == IBLB_PREC_F64)
+            HIP_TRY(c, launch_macro_out<double>(gptr<double>(c, c->cur), c->L, halo_of<double>(c, c->cur), fd, c->fplane,
+                                                c->coef.gx, c->coef.gy, (double*)dr.p, (double*)du.p, c->stream));
+        else
+            HIP_TRY(c, launch_macro_out<float>(gptr<float>(c, c->cur), c->L, halo_of<float>(c, c->cur), fd, c->fplane,
+                                               c->coef.gx, c->coef.gy, (double*)dr.p, (double*)du.p, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (rho) HIP_TRY(c, hipMemcpy(rho, dr.p, nb, hipMemcpyDeviceToHost));
+    if (u) HIP_TRY(c, hipMemcpy(u, du.p, 2 * nb, hipMemcpyDeviceToHost));
+    return IBLB_OK;
+}
+
+int iblb_get_populations(iblb_ctx* c, double* f) {
+    if (!c || !f) return IBLB_ERR_ARG;
+    int rc = prepare_read(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const long N = (long)c->ncol * c->ny;
+    DevBuf df;
+    HIP_TRY(c, hipMalloc(&df.p, 9 * (size_t)N * sizeof(double)));
+    const int raw = c->phase == PH_BOOT;  // f^0 is stored unstreamed
+    if (c->prec == IBLB_PREC_F64)
+        HIP_TRY(c, launch_pop_out<double>(gptr<double>(c, c->cur), c->L, halo_of<double>(c, c->cur), (double*)df.p,
+                                          raw, c->stream));
+    else
+        HIP_TRY(c, launch_pop_out<float>(gptr<float>(c, c->cur), c->L, halo_of<float>(c, c->cur), (double*)df.p, raw,
+                                         c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpy(f, df.p, 9 * (size_t)N * sizeof(double), hipMemcpyDeviceToHost));
+    return IBLB_OK;
+}
+
+int iblb_get_force(iblb_ctx* c, double* force) {
+    if (!c || !force) return IBLB_ERR_ARG;
+    int rc = prepare_read(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const long N = (long)c->ncol * c->ny;
+    DevBuf d;
+    HIP_TRY(c, hipMalloc(&d.p, 2 * (size_t)N * sizeof(double)));
+    if (c->phase == PH_BOOT)
+        HIP_TRY(c, launch_field_out(c->force0, (double*)d.p, c->L, 2, c->fplane, c->coef.gx, c->coef.gy, c->stream));
+    else
+        HIP_TRY(c, launch_field_out(c->ib_state == IB_READY ? c->fdense : nullptr, (double*)d.p, c->L, 2, c->fplane,
+                                    c->coef.gx, c->coef.gy, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpy(force, d.p, 2 * (size_t)N * sizeof(double), hipMemcpyDeviceToHost));
+    return IBLB_OK;
+}
+
+int iblb_get_lagrangian_force(iblb_ctx* c, float* F_s) {
+    if (!c || !F_s) return IBLB_ERR_ARG;
+    int rc = prepare_read(c);
+    if (rc) return rc;
+    if (c->ns == 0) return IBLB_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpy(F_s, c->d_Fs, 2 * (size_t)c->ns * sizeof(float), hipMemcpyDeviceToHost));
+    return IBLB_OK;
+}
+
+int iblb_get_flux(iblb_ctx* c, double* Q) {
+    if (!c || !Q) return IBLB_ERR_ARG;
+    int rc = prepare_read(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    // d_Q[1] = d_Q[0] + q(u^t) of the current (not yet collided) state
+    HIP_TRY(c, hipMemcpyAsync(c->d_Q + 1, c->d_Q, sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    const int fc = c->cfg.flux_column - c->x_begin;
+    if (c->phase == PH_RUN && fc >= 0 && fc < c->ncol) {
+        const double* fd = c->ib_state == IB_READY ? c->fdense : nullptr;
+        if (c->prec == IBLB_PREC_F64)
+            HIP_TRY(c, launch_flux<double>(gptr<double>(c, c->cur), c->L, halo_of<double>(c, c->cur), fd, c->fplane,
+                                           c->coef.gx, c->coef.gy, fc, c->cfg.flux_norm, c->d_Q + 1, c->stream));
+        else
+            HIP_TRY(c, launch_flux<float>(gptr<float>(c, c->cur), c->L, halo_of<float>(c, c->cur), fd, c->fplane,
+                                          c->coef.gx, c->coef.gy, fc, c->cfg.flux_norm, c->d_Q + 1, c->stream));
+    }
+    if (c->transport == TR_RCCL && c->nranks > 1)
+        NCCL_TRY(c, ncclAllReduce(c->d_Q + 1, c->d_Q + 1, 1, ncclFloat64, ncclSum, c->comm, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpy(Q, c->d_Q + 1, sizeof(double), hipMemcpyDeviceToHost));
+    return IBLB_OK;
+}
+
+int iblb_get_step(iblb_ctx* c, long long* steps) {
+    if (!c || !steps) return IBLB_ERR_ARG;
+    *steps = c->t;
+    return IBLB_OK;
+}
+
+int iblb_set_profiling(iblb_ctx* c, int enabled) {
+    if (!c) return IBLB_ERR_ARG;
+    c->prof = enabled != 0;
+    return IBLB_OK;
+}
+
+int iblb_get_timing(iblb_ctx* c, iblb_timing* t, int reset) {
+    if (!c || !t) return IBLB_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (auto& kv : c->ev_kind) {
+        float ms = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_pool[kv.second], c->ev_pool[kv.second + 1]));
+        if (kv.first == EV_FUSED) { c->fused_ms += ms; c->fused_launches++; }
+        else if (kv.first == EV_IB) c->ib_ms += ms;
+        else c->halo_ms += ms;
+    }
+    c->ev_kind.clear();
+    c->ev_used = 0;
+    t->steps = c->t;
+    t->fused_launches = c->fused_launches;
+    t->fused_ms = c->fused_ms;
+    t->ib_ms = c->ib_ms;
+    t->halo_ms = c->halo_ms;
+    t->fused_bytes = 18.0 * (double)c->esize;
+    t->cells = (long long)c->ncol * c->ny;
+    if (reset) {
+        c->fused_ms = c->ib_ms = c->halo_ms = 0.;
+        c->fused_launches = 0;
+    }
+    return IBLB_OK;
+}
+
+int iblb_get_stream(iblb_ctx* c, void** stream) {
+    if (!c || !stream) return IBLB_ERR_ARG;
+    *stream = (void*)c->stream;
+    return IBLB_OK;
+}
+
+int iblb_synchronize(iblb_ctx* c) {
+    if (!c) return IBLB_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return IBLB_OK;
+}
+
+// ---- local groups ---------------------------------------------------------------------------
+int iblb_link_local(iblb_ctx** ctxs, int n) {
+    if (!ctxs || n < 1) return IBLB_ERR_ARG;
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i]) return IBLB_ERR_ARG;
+        iblb_ctx* c = ctxs[i];
+        iblb_ctx* nx_ = ctxs[(i + 1) % n];
+        if (c->nx != ctxs[0]->nx || c->ny != ctxs[0]->ny || c->prec != ctxs[0]->prec)
+            return fail(c, IBLB_ERR_ARG, "local group: slabs differ in lattice size or precision");
+        if ((c->x_begin + c->ncol) % c->nx != nx_->x_begin)
+            return fail(c, IBLB_ERR_ARG, "local group: slabs must tile the lattice left to right");
+    }
+    long total = 0;
+    for (int i = 0; i < n; ++i) total += ctxs[i]->ncol;
+    if (total != ctxs[0]->nx) return fail(ctxs[0], IBLB_ERR_ARG, "local group: slabs do not cover the lattice");
+    if (n == 1) return IBLB_OK;  // a single slab is its own periodic neighbour
+    for (int i = 0; i < n; ++i) {
+        ctxs[i]->transport = TR_LOCAL;
+        ctxs[i]->left = ctxs[(i + n - 1) % n];
+        ctxs[i]->right = ctxs[(i + 1) % n];
+        ctxs[i]->halo_valid = false;
+    }
+    return IBLB_OK;
+}
+
+static int sync_all(iblb_ctx** cs, int n) {
+    for (int i = 0; i < n; ++i) {
+        HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
+        HIP_TRY(cs[i], hipStreamSynchronize(cs[i]->stream));
+    }
+    return IBLB_OK;
+}
+
+static int group_exchange(iblb_ctx** cs, int n) {
+    int rc = sync_all(cs, n);
+    if (rc) return rc;
+    for (int i = 0; i < n; ++i)
+        if ((rc = exchange_local(cs[i]))) return rc;
+    return sync_all(cs, n);
+}
+
+static int group_force(iblb_ctx** cs, int n) {
+    bool pending = false;
+    for (int i = 0; i < n; ++i) pending |= cs[i]->ib_state == IB_PENDING;
+    if (!pending) return IBLB_OK;
+    int rc;
+    for (int i = 0; i < n; ++i) {
+        HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
+        if ((rc = ib_nodes_any(cs[i]))) return rc;
+    }
+    if ((rc = sync_all(cs, n))) return rc;
+    // sum the per-slab node values (each node is owned by exactly one slab)
+    iblb_ctx* c0 = cs[0];
+    const size_t nb = 27 * (size_t)c0->ns * sizeof(double);
+    HIP_TRY(c0, hipSetDevice(c0->device));
+    for (int i = 1; i < n; ++i) {
+        HIP_TRY(c0, hipMemcpyAsync(c0->d_nv_tmp, cs[i]->d_nv, nb, hipMemcpyDefault, c0->stream));
+        HIP_TRY(c0, launch_sum_into(c0->d_nv, c0->d_nv_tmp, 27L * c0->ns, c0->stream));
+    }
+    HIP_TRY(c0, hipStreamSynchronize(c0->stream));
+    for (int i = 1; i < n; ++i) {
+        HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
+        HIP_TRY(cs[i], hipMemcpyAsync(cs[i]->d_nv, c0->d_nv, nb, hipMemcpyDefault, cs[i]->stream));
+    }
+    for (int i = 0; i < n; ++i) {
+        HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
+        if ((rc = ib_finish(cs[i]))) return rc;
+    }
+    return sync_all(cs, n);
+}
+
+int iblb_group_step(iblb_ctx** cs, int n, int nsteps) {
+    if (!cs || n < 1 || nsteps < 0) return IBLB_ERR_ARG;
+    if (n == 1) return iblb_step(cs[0], nsteps);
+    for (int i = 0; i < n; ++i) {
+        if (!cs[i] || cs[i]->transport != TR_LOCAL) return IBLB_ERR_ARG;
+        if (cs[i]->phase == PH_EMPTY) return fail(cs[i], IBLB_ERR_STATE, "no state: call iblb_set_state first");
+        if (cs[i]->phase != cs[0]->phase || cs[i]->t != cs[0]->t || cs[i]->ns != cs[0]->ns)
+            return fail(cs[i], IBLB_ERR_STATE, "local group: slabs out of step");
+    }
+    int rc;
+    for (int s = 0; s < nsteps; ++s) {
+        if (cs[0]->phase == PH_RUN) {
+            if (!cs[0]->halo_valid && (rc = group_exchange(cs, n))) return rc;
+            if ((rc = group_force(cs, n))) return rc;
+        }
+        for (int i = 0; i < n; ++i) {
+            HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
+            if ((rc = advance(cs[i]))) return rc;
+        }
+    }
+    // leave the group readable: halos of the new state and its force^t
+    if ((rc = group_exchange(cs, n))) return rc;
+    if ((rc = group_force(cs, n))) return rc;
+    for (int i = 0; i < n; ++i)
+        if (cs[i]->phase == PH_RUN && cs[i]->t >= 1 && cs[i]->rho0) free_boot(cs[i]);
+    return sync_all(cs, n);
+}
+
+// ---- RCCL groups ------------------------------------------------------------------------------
+int iblb_rccl_unique_id(char id[IBLB_UNIQUE_ID_BYTES]) {
+    if (!id) return IBLB_ERR_ARG;
+    static_assert(sizeof(ncclUniqueId) == IBLB_UNIQUE_ID_BYTES, "RCCL unique id size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return fail(nullptr, IBLB_ERR_COMM, "ncclGetUniqueId failed");
+    std::memcpy(id, &u, sizeof(u));
+    return IBLB_OK;
+}
+
+int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nranks, int rank) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return IBLB_ERR_ARG;
+    if (c->transport != TR_NONE) return fail(c, IBLB_ERR_STATE, "context already linked");
+    HIP_TRY(c, hipSetDevice(c->device));
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    NCCL_TRY(c, ncclCommInitRank(&c->comm, nranks, u, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    c->transport = TR_RCCL;
+    if (nranks > 1) {
+        // the slabs must tile the lattice in rank order: check (x_begin, ncol) of all ranks
+        DevBuf d;
+        HIP_TRY(c, hipMalloc(&d.p, 2 * sizeof(int) * (size_t)nranks));
+        int mine[2] = {c->x_begin, c->ncol};
+        HIP_TRY(c, hipMemcpy((int*)d.p + 2 * rank, mine, sizeof(mine), hipMemcpyHostToDevice));
+        NCCL_TRY(c, ncclAllGather((int*)d.p + 2 * rank, d.p, 2, ncclInt32, c->comm, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        std::vector<int> all(2 * (size_t)nranks);
+        HIP_TRY(c, hipMemcpy(all.data(), d.p, all.size() * sizeof(int), hipMemcpyDeviceToHost));
+        long total = 0;
+        for (int r = 0; r < nranks; ++r) {
+            total += all[2 * r + 1];
+            const int nxt = (r + 1) % nranks;
+            if ((all[2 * r] + all[2 * r + 1]) % c->nx != all[2 * nxt])
+                return fail(c, IBLB_ERR_ARG, "RCCL group: slabs must tile the lattice in rank order");
+        }
+        if (total != c->nx) return fail(c, IBLB_ERR_ARG, "RCCL group: slabs do not cover the lattice");
+    }
+    c->halo_valid = false;
+    return IBLB_OK;
+}
+
+}  // extern "C"

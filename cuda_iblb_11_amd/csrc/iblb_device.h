@@ -1,0 +1,192 @@
+// iblb_device.h — device-side building blocks of the MI355X IB-LBM hot path (gfx950).
+//
+// Lattice: D2Q9 with the reference's velocity order (LatticeBoltzmann.cu:15-27):
+//   i : 0      1      2      3       4       5      6       7        8
+//   c : (0,0)  (1,0)  (0,1)  (-1,0)  (0,-1)  (1,1)  (-1,1)  (-1,-1)  (1,-1)
+//   w : 4/9    1/9 x4                        1/36 x4
+//
+// Slab layout in HBM (one context = one x-slab [x_begin, x_begin+ncol)):
+//   g[i*plane + xc*col + y]  — SoA, one plane per direction, y fastest, column stride
+//   `col` (>= ny, multiple of 64 elements), planes padded apart.  A column is
+//   contiguous, so the halo a slab exchanges (one column, 3 planes) is 3 contiguous
+//   runs and needs no packing pass.
+//
+// State held between steps: post-collision populations f1^{t-1} ("g").  Streaming is a
+// PULL applied when g is read:
+//   f^t(x,y,k) = g(x-cx_k, y-cy_k, k)                  interior, x periodic
+//   f^t(x,0,k)    = g(x,0,bb(k))    k in {2,5,6}, bb = {4,7,8}   bounce-back
+//   f^t(x,Y-1,k)  = g(x,Y-1,sl(k))  k in {4,8,7}, sl = {2,5,6}   same-cell mirror
+// which is the reference's push streaming (LatticeBoltzmann.cu:173-373) read backwards.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace iblb {
+
+constexpr int Q9 = 9;
+__host__ __device__ constexpr int cx(int i) {
+    return i == 1 || i == 5 || i == 8 ? 1 : (i == 3 || i == 6 || i == 7 ? -1 : 0);
+}
+__host__ __device__ constexpr int cy(int i) {
+    return i == 2 || i == 5 || i == 6 ? 1 : (i == 4 || i == 7 || i == 8 ? -1 : 0);
+}
+__host__ __device__ constexpr double wgt(int i) {
+    return i == 0 ? 4. / 9 : (i < 5 ? 1. / 9 : 1. / 36);
+}
+// planes a slab receives from its LEFT neighbour (cx = +1) and from its RIGHT (cx = -1)
+__host__ __device__ constexpr int left_plane(int p) { return p == 0 ? 1 : (p == 1 ? 5 : 8); }
+__host__ __device__ constexpr int right_plane(int p) { return p == 0 ? 3 : (p == 1 ? 6 : 7); }
+__host__ __device__ constexpr int halo_slot(int k) {  // slot of plane k inside its halo triple
+    return (k == 1 || k == 3) ? 0 : ((k == 5 || k == 6) ? 1 : 2);
+}
+
+struct Layout {
+    int ny;      // lattice height Y
+    int ncol;    // columns in this slab
+    long col;    // column stride (elements)
+    long plane;  // plane stride (elements)
+};
+
+// Pointers to the three halo planes of column -1 (left, planes 1,5,8) and column
+// ncol (right, planes 3,6,7).  Single slab: they point into g itself (periodic wrap).
+template <typename T>
+struct Halo {
+    const T* left[3];
+    const T* right[3];
+};
+
+template <typename T>
+struct SendPtrs {
+    T* left[3];   // planes {3,6,7} of column 0
+    T* right[3];  // planes {1,5,8} of column ncol-1
+};
+
+// Relaxation and forcing constants shared by every collide.
+struct Coef {
+    double omega_p, omega_m;   // 1/TAU, 1/TAU2      (LatticeBoltzmann.cu:72-73)
+    double kguo;               // 1 - 1/(2 TAU)      (LatticeBoltzmann.cu:56)
+    double inv_cs2, inv_cs4;   // 1/C_S^2, 1/C_S^4 with C_S = 0.57735 (LatticeBoltzmann.cu:11)
+    double inv_2cs2, inv_2cs4; // 1/(2 C_S^2), 1/(2 C_S^4)
+    double gx, gy;             // uniform body force (extension, 0 in the reference)
+};
+
+// Scalar pull of f^t(xc, y, k) from g (used by every non-hot kernel).
+template <typename T>
+__device__ __forceinline__ T pull(const T* __restrict__ g, const Layout& L, const Halo<T>& H,
+                                  int xc, int y, int k) {
+    if (y == 0 && cy(k) == 1) {
+        const int kk = k == 2 ? 4 : (k == 5 ? 7 : 8);
+        return g[kk * L.plane + xc * L.col];
+    }
+    if (y == L.ny - 1 && cy(k) == -1) {
+        const int kk = k == 4 ? 2 : (k == 8 ? 5 : 6);
+        return g[kk * L.plane + xc * L.col + y];
+    }
+    const int sx = xc - cx(k), sy = y - cy(k);
+    if (sx < 0) return H.left[halo_slot(k)][sy];
+    if (sx >= L.ncol) return H.right[halo_slot(k)][sy];
+    return g[k * L.plane + (long)sx * L.col + sy];
+}
+
+// Storage conversion: double planes hold f, float planes hold the deviation f - w_i.
+template <typename T>
+struct Store;
+template <>
+struct Store<double> {
+    static constexpr bool dev = false;
+    __device__ __forceinline__ static double to_f(double v, int) { return v; }
+    __device__ __forceinline__ static double from_f(double v, int) { return v; }
+};
+template <>
+struct Store<float> {
+    static constexpr bool dev = true;
+    __device__ __forceinline__ static double to_f(float v, int i) { return (double)v + wgt(i); }
+    __device__ __forceinline__ static float from_f(double v, int i) { return (float)(v - wgt(i)); }
+};
+
+// Macroscopic moments of one cell in the reference's summation order
+// (LatticeBoltzmann.cu:396-405): rho = f0+...+f8, m = sum c f.  For deviation storage
+// `rho` returns sum h (= rho - 1); the caller adds 1.
+template <typename R>
+__device__ __forceinline__ void moments(const R f[9], R& rho, R& mx, R& my) {
+    rho = f[0] + f[1] + f[2] + f[3] + f[4] + f[5] + f[6] + f[7] + f[8];
+    mx = ((((f[1] - f[3]) + f[5]) - f[6]) - f[7]) + f[8];
+    my = ((((f[2] - f[4]) + f[5]) + f[6]) - f[7]) - f[8];
+}
+
+// TRT collision with the reference's Guo forcing (LatticeBoltzmann.cu:30-62, 64-171)
+// written on the even/odd parts of each pair:
+//   feq+ = rho w (1 + (c.u)^2/(2cs^4) - u^2/(2cs^2)),   feq- = rho w (c.u)/cs^2
+//   F+   = k w (-(u.F)/cs^2 + (c.u)(c.F)/cs^4),          F-   = k w (c.F)/cs^2
+//   f1_i = f_i - w+ (f+ - feq+) + F+  -  w- (f- - feq-) + F-
+//   f1_ibar = f_ibar - w+ (f+ - feq+) + F+ + w- (f- - feq-) - F-
+//   f1_0 = f_0 - w+ (f_0 - feq_0)                         (no F_0, as in the reference)
+// Algebraically identical to the reference; rounding differs at the 1e-16 level.
+// DEV: f holds deviations h = f - w and drho = rho - 1 (float storage).
+template <typename R, bool DEV>
+__device__ __forceinline__ void collide(R f[9], R rho, R drho, R ux, R uy, R Fx, R Fy, const Coef& c) {
+    const R op = (R)c.omega_p, om = (R)c.omega_m;
+    const R a1 = (R)c.inv_2cs2, a2 = (R)c.inv_2cs4, ics2 = (R)c.inv_cs2, ics4 = (R)c.inv_cs4;
+    const R usq = ux * ux + uy * uy;
+    const R uF = ux * Fx + uy * Fy;
+    const R base = -usq * a1;  // even equilibrium part common to all i
+    const R kk = (R)c.kguo;
+    // rest population
+    {
+        const R w0 = (R)(4. / 9);
+        const R feq0 = DEV ? w0 * (drho + rho * base) : rho * w0 * ((R)1 + base);
+        f[0] = f[0] - op * (f[0] - feq0);
+    }
+    const R guF = -uF * ics2;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int a = p == 0 ? 1 : (p == 1 ? 2 : (p == 2 ? 5 : 6));
+        const int b = p == 0 ? 3 : (p == 1 ? 4 : (p == 2 ? 7 : 8));
+        const R w = (R)wgt(a);
+        const R cu = (R)cx(a) * ux + (R)cy(a) * uy;
+        const R cF = (R)cx(a) * Fx + (R)cy(a) * Fy;
+        const R rw = rho * w;
+        const R feqp = DEV ? w * drho + rw * (base + cu * cu * a2) : rw * ((R)1 + base + cu * cu * a2);
+        const R feqm = rw * cu * ics2;
+        const R fp = (R)0.5 * (f[a] + f[b]);
+        const R fm = (R)0.5 * (f[a] - f[b]);
+        const R kw = kk * w;
+        const R Gp = kw * (guF + cu * cF * ics4);
+        const R Gm = kw * cF * ics2;
+        const R A = -op * (fp - feqp) + Gp;
+        const R B = -om * (fm - feqm) + Gm;
+        f[a] = f[a] + A + B;
+        f[b] = f[b] + A - B;
+    }
+}
+
+// ImmersedBoundary.cu:21-81, with the reference's float/double rounding points.
+// Compiled with contraction off so it matches the C restatement bit for bit.
+__device__ __forceinline__ float d_delta(float xs, float ys, int x, int y) {
+#pragma clang fp contract(off)
+    float dx = fabsf((float)x - xs);
+    float dy = fabsf((float)y - ys);
+    double a = 0., b = 0., d = 0.;
+    int c = 0;
+    if (dx <= 1.5f) {
+        if (dx <= 0.5f) { a = 0.33333; b = 1.; c = 1; d = dx; }
+        else { a = 0.16667; b = 5. - 3. * (double)dx; c = -1; d = (double)(1.f - dx); }
+    }
+    const float deltax = (float)(a * (b + (double)c * sqrt(-3. * d * d + 1.)));
+    a = 0.; b = 0.; c = 0; d = 0.;
+    if (dy <= 1.5f) {
+        if (dy <= 0.5f) { a = 0.33333; b = 1.; c = 1; d = dy; }
+        else { a = 0.16667; b = 5. - 3. * (double)dy; c = -1; d = (double)(1.f - dy); }
+    }
+    const float deltay = (float)(a * (b + (double)c * sqrt(-3. * d * d + 1.)));
+    return deltax * deltay;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace iblb

@@ -1,0 +1,82 @@
+// iblb_kernels.h — host-callable launchers of the slab kernels (used by iblb_ctx.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "iblb_device.h"
+
+namespace iblb {
+
+// Cells per lane of the collide-stream kernel: 16 bytes per lane per plane.
+template <typename T>
+constexpr int vec_of() { return 16 / (int)sizeof(T); }
+
+template <typename T>
+struct FusedArgs {
+    const T* src;
+    T* dst;
+    Layout L;
+    Halo<T> H;
+    T* send_left[3];    // planes {3,6,7} of column 0 (nullptr = not sent)
+    T* send_right[3];   // planes {1,5,8} of column ncol-1
+    int col_begin;      // first local column handled by this launch
+    int ncols;          // columns handled by this launch
+    int nch;            // 64*V-row chunks per column
+    const uint8_t* flags;  // per (column, chunk): dense IB force present (nullptr: no IB)
+    double* fdense;     // dense IB force, x plane then y plane (same col stride)
+    long fplane;
+    int flux_col;       // local column sampled for Q, or -1
+    double flux_norm;
+    double* Q;
+    Coef c;
+};
+
+// Launch geometry of the collide-stream kernel: one wave per (column, 64*V-row chunk).
+inline int chunks_per_column(int ny, int V) { return (ny + 64 * V - 1) / (64 * V); }
+
+template <typename T>
+hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s);
+
+// Step 0 of a fresh state: collide f^0 with explicit rho^0, u^0, force^0 (no pull).
+template <typename T>
+hipError_t launch_boot(const T* src, T* dst, Layout L, const double* rho0, const double* u0,
+                       const double* force0, long fplane, T* const send_left[3], T* const send_right[3],
+                       Coef c, hipStream_t s);
+
+// Macroscopic output in the reference layout (slab-local j = y*ncol + xc):
+// rho = sum f, u = (sum c f + force/2)/rho with force = g + dense IB force.
+template <typename T>
+hipError_t launch_macro_out(const T* g, Layout L, Halo<T> H, const double* fdense, long fplane,
+                            double gx, double gy, double* rho, double* u, hipStream_t s);
+
+// Post-stream populations f^t in the reference AoS layout [9*j+i] (raw: no pull).
+template <typename T>
+hipError_t launch_pop_out(const T* g, Layout L, Halo<T> H, double* f, int raw, hipStream_t s);
+
+// q(u^t) of the current state for the flux column (added to *out).
+template <typename T>
+hipError_t launch_flux(const T* g, Layout L, Halo<T> H, const double* fdense, long fplane,
+                       double gx, double gy, int xc, double flux_norm, double* out, hipStream_t s);
+
+// Reference AoS populations [9*j+i] -> slab planes (deviation form for float).
+template <typename T>
+hipError_t launch_pop_in(const double* f, T* g, Layout L, hipStream_t s);
+
+// Reference SoA field [comp*N + j] (j = y*ncol + xc) <-> slab layout [comp*fplane + xc*col + y].
+hipError_t launch_field_in(const double* ref, double* lay, Layout L, int ncomp, long fplane, hipStream_t s);
+hipError_t launch_field_out(const double* lay, double* ref, Layout L, int ncomp, long fplane, double add0,
+                            double add1, hipStream_t s);
+
+// Immersed boundary (global coordinates; the slab owns columns [x_begin, x_begin+ncol)).
+template <typename T>
+hipError_t launch_ib_nodes(const T* g, Layout L, Halo<T> H, int nx, int x_begin, int ns, const float* s,
+                           double* node_vals, hipStream_t st);
+hipError_t launch_ib_interp(int nx, int ny, int ns, const float* s, const float* u_s, const double* node_vals,
+                            float* F_s, hipStream_t st);
+hipError_t launch_ib_spread(Layout L, int nx, int x_begin, int ns, const float* s, const float* F_s,
+                            const int* eps, double* fdense, long fplane, uint8_t* flags, int nch,
+                            int rows_per_chunk, hipStream_t st);
+hipError_t launch_sum_into(double* dst, const double* src, long n, hipStream_t st);
+
+}  // namespace iblb

@@ -1,0 +1,360 @@
+// lbm_kernels.hip — fused pull-stream + TRT/Guo collide for gfx950, and the slab
+// support kernels (boot step, macro/population/flux readers, layout conversion).
+//
+// Hot kernel: fused_kernel.  Per lattice update it reads the 9 populations once and
+// writes them once: 144 B/LU in double, 72 B/LU in float (algorithmic minimum).
+// Reference data flow it replaces: equilibrium -> collision -> streaming -> macro ->
+// spread's u correction (LatticeBoltzmann.cu:30-411, ImmersedBoundary.cu:249-264),
+// ~824 B/LU there.
+#include "iblb_kernels.h"
+
+namespace iblb {
+
+namespace {
+
+template <typename T, int V>
+struct VT {
+    typedef T type __attribute__((ext_vector_type(V)));
+};
+
+// 16-byte load at a 16-byte aligned address.
+template <typename T, int V>
+__device__ __forceinline__ typename VT<T, V>::type lda(const T* p) {
+    return *reinterpret_cast<const typename VT<T, V>::type*>(p);
+}
+// 16-byte load at an element-aligned (misaligned by one element) address.
+template <typename T, int V>
+__device__ __forceinline__ typename VT<T, V>::type ldu(const T* p) {
+    typename VT<T, V>::type r;
+    __builtin_memcpy(&r, p, sizeof(r));
+    return r;
+}
+template <typename T, int V>
+__device__ __forceinline__ void sta(T* p, typename VT<T, V>::type v) {
+    *reinterpret_cast<typename VT<T, V>::type*>(p) = v;
+}
+
+// Compute type: double storage collides in double, float storage in float
+// (deviation form keeps rho ~ 1 out of the float mantissa).
+template <typename T>
+struct Calc { typedef double R; };
+template <>
+struct Calc<float> { typedef float R; };
+
+}  // namespace
+
+// One wave = one (column, chunk of 64*V rows); lane l owns rows y0 .. y0+V-1.
+// Column-uniform decisions (halo source, flux column, IB flag, send buffers) are
+// scalar branches.  Walls are per-lane fixes of the first / last row.
+template <typename T, int V, bool IB>
+__global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
+    typedef typename VT<T, V>::type vec;
+    typedef typename Calc<T>::R R;
+    constexpr bool DEV = Store<T>::dev;
+    const int lane = threadIdx.x & 63;
+    const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (gw >= a.ncols * a.nch) return;
+    const int xc = a.col_begin + gw / a.nch;
+    const int ch = gw - (gw / a.nch) * a.nch;
+    const Layout L = a.L;
+    const int y0 = ch * (64 * V) + lane * V;
+    const long cb = (long)xc * L.col;
+    const T* __restrict__ src = a.src;
+
+    const T* p0 = src + cb;
+    const T* p2 = src + 2 * L.plane + cb;
+    const T* p4 = src + 4 * L.plane + cb;
+    const T *p1, *p5, *p8, *p3, *p6, *p7;
+    if (xc == 0) {
+        p1 = a.H.left[0]; p5 = a.H.left[1]; p8 = a.H.left[2];
+    } else {
+        p1 = src + 1 * L.plane + cb - L.col; p5 = src + 5 * L.plane + cb - L.col; p8 = src + 8 * L.plane + cb - L.col;
+    }
+    if (xc == L.ncol - 1) {
+        p3 = a.H.right[0]; p6 = a.H.right[1]; p7 = a.H.right[2];
+    } else {
+        p3 = src + 3 * L.plane + cb + L.col; p6 = src + 6 * L.plane + cb + L.col; p7 = src + 7 * L.plane + cb + L.col;
+    }
+
+    // pull: cy = 0 planes aligned, cy = +1 planes from row y-1, cy = -1 planes from row y+1
+    vec v0 = lda<T, V>(p0 + y0);
+    vec v1 = lda<T, V>(p1 + y0);
+    vec v3 = lda<T, V>(p3 + y0);
+    vec v2 = ldu<T, V>(p2 + y0 - 1);
+    vec v5 = ldu<T, V>(p5 + y0 - 1);
+    vec v6 = ldu<T, V>(p6 + y0 - 1);
+    vec v4 = ldu<T, V>(p4 + y0 + 1);
+    vec v7 = ldu<T, V>(p7 + y0 + 1);
+    vec v8 = ldu<T, V>(p8 + y0 + 1);
+    if (y0 == 0) {  // bounce-back on y = 0 (LatticeBoltzmann.cu:328-340)
+        v2[0] = src[4 * L.plane + cb];
+        v5[0] = src[7 * L.plane + cb];
+        v6[0] = src[8 * L.plane + cb];
+    }
+    const int et = L.ny - 1 - y0;
+    if (et >= 0 && et < V) {  // same-cell mirror on y = Y-1 (LatticeBoltzmann.cu:341-353)
+        const long top = cb + L.ny - 1;
+        const T t2 = src[2 * L.plane + top], t5 = src[5 * L.plane + top], t6 = src[6 * L.plane + top];
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+            if (e == et) { v4[e] = t2; v8[e] = t5; v7[e] = t6; }
+    }
+
+    // dense IB force for this (column, chunk), consumed and cleared
+    bool has_f = false;
+    if (IB) has_f = a.flags[(long)xc * a.nch + ch] != 0;
+    double fxv[V], fyv[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { fxv[e] = 0.; fyv[e] = 0.; }
+    if (IB && has_f) {
+        double* fx = a.fdense + cb + y0;
+        double* fy = a.fdense + a.fplane + cb + y0;
+#pragma unroll
+        for (int e = 0; e < V; ++e) { fxv[e] = fx[e]; fyv[e] = fy[e]; fx[e] = 0.; fy[e] = 0.; }
+    }
+
+    const bool do_flux = xc == a.flux_col;
+    double q = 0.;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+        R f[9] = {(R)v0[e], (R)v1[e], (R)v2[e], (R)v3[e], (R)v4[e], (R)v5[e], (R)v6[e], (R)v7[e], (R)v8[e]};
+        R s, mx, my;
+        moments<R>(f, s, mx, my);
+        const R rho = DEV ? (R)1 + s : s;
+        const R Fx = (R)(a.c.gx + fxv[e]);
+        const R Fy = (R)(a.c.gy + fyv[e]);
+        const R inv = (R)1 / rho;
+        const R ux = (mx + (R)0.5 * Fx) * inv;
+        const R uy = (my + (R)0.5 * Fy) * inv;
+        if (do_flux && y0 + e < L.ny) q += (double)ux / a.flux_norm;
+        collide<R, DEV>(f, rho, s, ux, uy, Fx, Fy, a.c);
+        v0[e] = (T)f[0]; v1[e] = (T)f[1]; v2[e] = (T)f[2]; v3[e] = (T)f[3]; v4[e] = (T)f[4];
+        v5[e] = (T)f[5]; v6[e] = (T)f[6]; v7[e] = (T)f[7]; v8[e] = (T)f[8];
+    }
+    T* dst = a.dst + cb + y0;
+    sta<T, V>(dst, v0);
+    sta<T, V>(dst + 1 * L.plane, v1);
+    sta<T, V>(dst + 2 * L.plane, v2);
+    sta<T, V>(dst + 3 * L.plane, v3);
+    sta<T, V>(dst + 4 * L.plane, v4);
+    sta<T, V>(dst + 5 * L.plane, v5);
+    sta<T, V>(dst + 6 * L.plane, v6);
+    sta<T, V>(dst + 7 * L.plane, v7);
+    sta<T, V>(dst + 8 * L.plane, v8);
+    if (xc == 0 && a.send_left[0]) {
+        sta<T, V>(a.send_left[0] + y0, v3);
+        sta<T, V>(a.send_left[1] + y0, v6);
+        sta<T, V>(a.send_left[2] + y0, v7);
+    }
+    if (xc == L.ncol - 1 && a.send_right[0]) {
+        sta<T, V>(a.send_right[0] + y0, v1);
+        sta<T, V>(a.send_right[1] + y0, v5);
+        sta<T, V>(a.send_right[2] + y0, v8);
+    }
+    if (do_flux) {
+        q = wave_sum(q);
+        if (lane == 0) atomicAdd(a.Q, q);
+    }
+}
+
+template <typename T>
+hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s) {
+    constexpr int V = vec_of<T>();
+    const long waves = (long)a.ncols * a.nch;
+    if (waves <= 0) return hipSuccess;
+    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    if (a.flags)
+        fused_kernel<T, V, true><<<blocks, 256, 0, s>>>(a);
+    else
+        fused_kernel<T, V, false><<<blocks, 256, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+// ---- boot step: collide f^0 with given rho^0, u^0, force^0 (main.cu:720-754, it = 0) --
+template <typename T>
+__global__ __launch_bounds__(256) void boot_kernel(const T* __restrict__ src, T* __restrict__ dst, Layout L,
+                                                   const double* __restrict__ rho0, const double* __restrict__ u0,
+                                                   const double* __restrict__ force0, long fplane, SendPtrs<T> sp,
+                                                   Coef c) {
+    typedef typename Calc<T>::R R;
+    constexpr bool DEV = Store<T>::dev;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long)L.ncol * L.ny) return;
+    const int xc = (int)(idx / L.ny), y = (int)(idx - (long)xc * L.ny);
+    const long o = (long)xc * L.col + y;
+    R f[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) f[i] = (R)src[i * L.plane + o];
+    const double rho = rho0[o];
+    const R ux = (R)u0[o], uy = (R)u0[fplane + o];
+    const R Fx = (R)(c.gx + (force0 ? force0[o] : 0.)), Fy = (R)(c.gy + (force0 ? force0[fplane + o] : 0.));
+    collide<R, DEV>(f, (R)rho, (R)(rho - 1.0), ux, uy, Fx, Fy, c);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) dst[i * L.plane + o] = (T)f[i];
+    if (xc == 0 && sp.left[0]) { sp.left[0][y] = (T)f[3]; sp.left[1][y] = (T)f[6]; sp.left[2][y] = (T)f[7]; }
+    if (xc == L.ncol - 1 && sp.right[0]) { sp.right[0][y] = (T)f[1]; sp.right[1][y] = (T)f[5]; sp.right[2][y] = (T)f[8]; }
+}
+
+template <typename T>
+hipError_t launch_boot(const T* src, T* dst, Layout L, const double* rho0, const double* u0, const double* force0,
+                       long fplane, T* const send_left[3], T* const send_right[3], Coef c, hipStream_t s) {
+    SendPtrs<T> sp;
+    for (int p = 0; p < 3; ++p) { sp.left[p] = send_left[p]; sp.right[p] = send_right[p]; }
+    const long n = (long)L.ncol * L.ny;
+    boot_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(src, dst, L, rho0, u0, force0, fplane, sp, c);
+    return hipGetLastError();
+}
+
+// ---- readers ------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void pull_cell(const T* g, const Layout& L, const Halo<T>& H, int xc, int y, double f[9]) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = Store<T>::to_f(pull<T>(g, L, H, xc, y, k), k);
+}
+
+// rho = sum f in the reference order (LatticeBoltzmann.cu:396-399); u corrected as in
+// ImmersedBoundary.cu:249-255.  Contraction off: matches the C restatement bit for bit
+// given the same populations.
+template <typename T>
+__global__ void macro_out_kernel(const T* __restrict__ g, Layout L, Halo<T> H, const double* __restrict__ fdense,
+                                 long fplane, double gx, double gy, double* __restrict__ rho_out,
+                                 double* __restrict__ u_out) {
+#pragma clang fp contract(off)
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long N = (long)L.ncol * L.ny;
+    if (idx >= N) return;
+    const int y = (int)(idx / L.ncol), xc = (int)(idx - (long)y * L.ncol);  // reference order j = y*ncol + xc
+    double f[9];
+    pull_cell<T>(g, L, H, xc, y, f);
+    double r, mx, my;
+    moments<double>(f, r, mx, my);
+    const long o = (long)xc * L.col + y;
+    const double Fx = (fdense ? fdense[o] : 0.) + gx;
+    const double Fy = (fdense ? fdense[fplane + o] : 0.) + gy;
+    if (rho_out) rho_out[idx] = r;
+    if (u_out) {
+        u_out[idx] = (mx + 0.5 * Fx) / r;
+        u_out[N + idx] = (my + 0.5 * Fy) / r;
+    }
+}
+
+template <typename T>
+hipError_t launch_macro_out(const T* g, Layout L, Halo<T> H, const double* fdense, long fplane, double gx, double gy,
+                            double* rho, double* u, hipStream_t s) {
+    const long n = (long)L.ncol * L.ny;
+    macro_out_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(g, L, H, fdense, fplane, gx, gy, rho, u);
+    return hipGetLastError();
+}
+
+// raw != 0: g holds unstreamed f^0 (boot phase), read each cell in place.
+template <typename T>
+__global__ void pop_out_kernel(const T* __restrict__ g, Layout L, Halo<T> H, double* __restrict__ f_out, int raw) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long)L.ncol * L.ny) return;
+    const int y = (int)(idx / L.ncol), xc = (int)(idx - (long)y * L.ncol);
+    double f[9];
+    if (raw) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) f[k] = Store<T>::to_f(g[k * L.plane + (long)xc * L.col + y], k);
+    } else {
+        pull_cell<T>(g, L, H, xc, y, f);
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f_out[9 * idx + k] = f[k];
+}
+
+template <typename T>
+hipError_t launch_pop_out(const T* g, Layout L, Halo<T> H, double* f, int raw, hipStream_t s) {
+    const long n = (long)L.ncol * L.ny;
+    pop_out_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(g, L, H, f, raw);
+    return hipGetLastError();
+}
+
+template <typename T>
+__global__ void flux_kernel(const T* __restrict__ g, Layout L, Halo<T> H, const double* __restrict__ fdense,
+                            long fplane, double gx, double gy, int xc, double flux_norm, double* out) {
+#pragma clang fp contract(off)
+    double q = 0.;
+    for (int y = threadIdx.x; y < L.ny; y += blockDim.x) {
+        double f[9];
+        pull_cell<T>(g, L, H, xc, y, f);
+        double r, mx, my;
+        moments<double>(f, r, mx, my);
+        const long o = (long)xc * L.col + y;
+        const double Fx = (fdense ? fdense[o] : 0.) + gx;
+        q += ((mx + 0.5 * Fx) / r) / flux_norm;
+    }
+    q = wave_sum(q);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, q);
+}
+
+template <typename T>
+hipError_t launch_flux(const T* g, Layout L, Halo<T> H, const double* fdense, long fplane, double gx, double gy, int xc,
+                       double flux_norm, double* out, hipStream_t s) {
+    flux_kernel<T><<<1, 256, 0, s>>>(g, L, H, fdense, fplane, gx, gy, xc, flux_norm, out);
+    return hipGetLastError();
+}
+
+// ---- layout conversion ------------------------------------------------------------------
+template <typename T>
+__global__ void pop_in_kernel(const double* __restrict__ f, T* __restrict__ g, Layout L) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long)L.ncol * L.ny) return;
+    const int y = (int)(idx / L.ncol), xc = (int)(idx - (long)y * L.ncol);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) g[k * L.plane + (long)xc * L.col + y] = Store<T>::from_f(f[9 * idx + k], k);
+}
+
+template <typename T>
+hipError_t launch_pop_in(const double* f, T* g, Layout L, hipStream_t s) {
+    const long n = (long)L.ncol * L.ny;
+    pop_in_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(f, g, L);
+    return hipGetLastError();
+}
+
+__global__ void field_in_kernel(const double* __restrict__ ref, double* __restrict__ lay, Layout L, int ncomp, long fplane) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long N = (long)L.ncol * L.ny;
+    if (idx >= N) return;
+    const int y = (int)(idx / L.ncol), xc = (int)(idx - (long)y * L.ncol);
+    for (int a = 0; a < ncomp; ++a) lay[a * fplane + (long)xc * L.col + y] = ref[a * N + idx];
+}
+
+__global__ void field_out_kernel(const double* __restrict__ lay, double* __restrict__ ref, Layout L, int ncomp,
+                                 long fplane, double add0, double add1) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long N = (long)L.ncol * L.ny;
+    if (idx >= N) return;
+    const int y = (int)(idx / L.ncol), xc = (int)(idx - (long)y * L.ncol);
+    for (int a = 0; a < ncomp; ++a)
+        ref[a * N + idx] = (lay ? lay[a * fplane + (long)xc * L.col + y] : 0.) + (a == 0 ? add0 : add1);
+}
+
+hipError_t launch_field_in(const double* ref, double* lay, Layout L, int ncomp, long fplane, hipStream_t s) {
+    const long n = (long)L.ncol * L.ny;
+    field_in_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(ref, lay, L, ncomp, fplane);
+    return hipGetLastError();
+}
+
+hipError_t launch_field_out(const double* lay, double* ref, Layout L, int ncomp, long fplane, double add0, double add1,
+                            hipStream_t s) {
+    const long n = (long)L.ncol * L.ny;
+    field_out_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(lay, ref, L, ncomp, fplane, add0, add1);
+    return hipGetLastError();
+}
+
+#define IBLB_INST(T)                                                                                            \
+    template hipError_t launch_fused<T>(const FusedArgs<T>&, hipStream_t);                                      \
+    template hipError_t launch_boot<T>(const T*, T*, Layout, const double*, const double*, const double*, long,  \
+                                       T* const[3], T* const[3], Coef, hipStream_t);                            \
+    template hipError_t launch_macro_out<T>(const T*, Layout, Halo<T>, const double*, long, double, double,      \
+                                            double*, double*, hipStream_t);                                     \
+    template hipError_t launch_pop_out<T>(const T*, Layout, Halo<T>, double*, int, hipStream_t);                     \
+    template hipError_t launch_flux<T>(const T*, Layout, Halo<T>, const double*, long, double, double, int,      \
+                                       double, double*, hipStream_t);                                           \
+    template hipError_t launch_pop_in<T>(const double*, T*, Layout, hipStream_t);
+
+IBLB_INST(double)
+IBLB_INST(float)
+
+}  // namespace iblb

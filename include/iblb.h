@@ -1,0 +1,194 @@
+/*
+ * iblb.h — C ABI of the MI355X-native immersed-boundary lattice-Boltzmann hot path.
+ *
+ * Replaces the hot path of ptheywood/CUDA_IBLB_11 (reference @ /root/reference):
+ *   LatticeBoltzmann.cuh:4-10  equilibrium / collision / streaming / macro kernels
+ *   ImmersedBoundary.cuh:4-8   interpolate / spread kernels
+ *   main.cu:817-934            the per-step launch sequence that drives them
+ *
+ * Two layers are exported:
+ *
+ *  (1) Reference-shaped entry points (iblb_equilibrium ... iblb_spread).  Same names,
+ *      same argument lists and the same array layouts as the reference kernels
+ *      (device pointers; f/f0/f1/F are AoS [9*j+i], u/force are SoA [a*size+j],
+ *      Lagrangian arrays are interleaved float xy), plus a trailing HIP stream.
+ *      A maintainer replaces `kernel<<<grid, block, 0, s>>>(args)` in main.cu by
+ *      `iblb_kernel(args, s)`.  They keep the reference's unfused data flow and exist
+ *      for drop-in compatibility and kernel-by-kernel parity, not for speed.
+ *
+ *  (2) The fused context API (iblb_create ... iblb_destroy).  One context owns one
+ *      x-slab of the lattice on one GPU, stores the populations SoA (y fastest) and
+ *      advances the exact reference time step
+ *        equilibrium -> collision -> streaming -> macro -> interpolate -> spread
+ *      (main.cu:852-909) with ONE bandwidth-bound kernel per step plus tiny IB
+ *      kernels.  Host arrays crossing this boundary use the reference layouts
+ *      restricted to the slab: cell j = y * x_count + (x - x_begin).
+ *
+ * Conventions: every function returns IBLB_OK (0) or a negative IBLB_ERR_* code;
+ * no C++ exception crosses the ABI.  The caller owns host buffers, the library owns
+ * device buffers.  One host thread per context.  Context calls are synchronous on
+ * return (results are in the caller's buffers).  The reference had no error
+ * channel other than cudaGetLastError() at the call sites (main.cu:724-728,
+ * 854-887, 902-922); here the code is returned and iblb_last_error() explains it.
+ */
+#ifndef IBLB_H
+#define IBLB_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IBLB_OK               0
+#define IBLB_ERR_ARG         -1   /* invalid argument / shape                      */
+#define IBLB_ERR_HIP         -2   /* HIP runtime error (message in last_error)     */
+#define IBLB_ERR_STATE       -3   /* call not valid in the current context state   */
+#define IBLB_ERR_COMM        -4   /* RCCL / transport error                        */
+#define IBLB_ERR_NOMEM       -5   /* device or host allocation failed              */
+#define IBLB_ERR_UNSUPPORTED -6   /* feature not built / not available             */
+#define IBLB_ERR_NODEVICE    -7   /* no HIP device visible                         */
+
+#define IBLB_PREC_F64 0          /* populations stored and collided in double      */
+#define IBLB_PREC_F32 1          /* populations stored as float deviations f - w_i */
+
+#define IBLB_UNIQUE_ID_BYTES 128 /* size of the RCCL unique id blob               */
+
+/* ---------------------------------------------------------------------------------
+ * (1) Reference-shaped kernels.  All pointers are DEVICE pointers.  `stream` is a
+ * hipStream_t (NULL = default stream).  Launch is asynchronous, like the reference's
+ * <<< >>> launches; the return value reports launch errors only.
+ * ------------------------------------------------------------------------------- */
+
+/* LatticeBoltzmann.cu:30 equilibrium(u, rho, f0, force, F, XDIM, YDIM, TAU) */
+int iblb_equilibrium(const double* u, const double* rho, double* f0, const double* force,
+                     double* F, int XDIM, int YDIM, double TAU, void* stream);
+
+/* LatticeBoltzmann.cu:64 collision(f0, f, f1, F, TAU, TAU2, XDIM, YDIM, it) — `it` unused as in the reference */
+int iblb_collision(const double* f0, const double* f, double* f1, const double* F,
+                   double TAU, double TAU2, int XDIM, int YDIM, int it, void* stream);
+
+/* LatticeBoltzmann.cu:173 streaming(f1, f, XDIM, YDIM) */
+int iblb_streaming(const double* f1, double* f, int XDIM, int YDIM, void* stream);
+
+/* LatticeBoltzmann.cu:375 macro(f, u, rho, XDIM, YDIM) */
+int iblb_macro(const double* f, double* u, double* rho, int XDIM, int YDIM, void* stream);
+
+/* ImmersedBoundary.cu:94 interpolate(rho, u, Ns, u_s, F_s, s, XDIM, YDIM) */
+int iblb_interpolate(const double* rho, const double* u, int Ns, const float* u_s, float* F_s,
+                     const float* s, int XDIM, int YDIM, void* stream);
+
+/* ImmersedBoundary.cu:138 spread(rho, u, f, Ns, u_s, F_s, force, s, XDIM, Q, epsilon).
+ * Like the reference it assumes YDIM == 192 (`size = 192 * XDIM`, ImmersedBoundary.cu:146)
+ * and accumulates Q += u_x(XDIM-5, y)/192 (ImmersedBoundary.cu:259-264). */
+int iblb_spread(const double* rho, double* u, const double* f, int Ns, const float* u_s,
+                const float* F_s, double* force, const float* s, int XDIM, double* Q,
+                const int* epsilon, void* stream);
+
+/* spread with the grid height, flux column and flux divisor made explicit
+ * (YDIM == 192, flux_column == XDIM-5, flux_norm == 192 reproduces iblb_spread). */
+int iblb_spread_ex(const double* rho, double* u, const double* f, int Ns, const float* u_s,
+                   const float* F_s, double* force, const float* s, int XDIM, int YDIM,
+                   double* Q, const int* epsilon, int flux_column, double flux_norm,
+                   void* stream);
+
+/* ImmersedBoundary.cu:21 d_delta, evaluated on the device for n (xs, ys, x, y) tuples
+ * (parity hook for the 3-point kernel). */
+int iblb_delta(int n, const float* xs, const float* ys, const int* x, const int* y,
+               float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * (2) Fused context API.
+ * ------------------------------------------------------------------------------- */
+
+typedef struct iblb_ctx iblb_ctx;
+
+typedef struct iblb_config {
+    int    nx, ny;            /* global lattice XDIM x YDIM (main.cu:270-271,298)          */
+    double tau, tau2;         /* TAU, TAU2 (main.cu:320-321)                               */
+    int    precision;         /* IBLB_PREC_F64 (default) or IBLB_PREC_F32                  */
+    double body_force[2];     /* uniform force added to force^t every step; (0,0) = ref.  */
+    double flux_norm;         /* Q += u_x / flux_norm; reference literal 192 (IB.cu:261)   */
+    int    flux_column;       /* global column sampled for Q; reference XDIM-5 (IB.cu:259) */
+    int    device;            /* HIP device ordinal                                        */
+    int    x_begin, x_count;  /* owned columns [x_begin, x_begin + x_count); x_count <= 0
+                                 means the whole lattice (single slab)                     */
+    int    max_points;        /* Lagrangian point capacity; 0 disables the IB kernels      */
+} iblb_config;
+
+typedef struct iblb_timing {
+    long long steps;           /* reference steps completed                              */
+    long long fused_launches;  /* collide-stream launches timed                          */
+    double    fused_ms;        /* summed duration of the timed collide-stream launches   */
+    double    ib_ms;           /* summed duration of IB phases (interp + spread)         */
+    double    halo_ms;         /* summed duration of halo exchanges                      */
+    double    fused_bytes;     /* algorithmic bytes per cell of the collide-stream kernel */
+    long long cells;           /* cells owned by this context                            */
+} iblb_timing;
+
+/* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */
+int iblb_config_default(iblb_config* cfg);
+
+int  iblb_create(const iblb_config* cfg, iblb_ctx** out);
+void iblb_destroy(iblb_ctx* ctx);
+const char* iblb_last_error(const iblb_ctx* ctx);   /* NULL ctx: last create() error */
+const char* iblb_version(void);
+int  iblb_device_count(int* n);
+
+/* Initial state (main.cu:636-754).  rho [N], u [2N] SoA, force [2N] SoA (force^0, may be
+ * NULL = 0), f [9N] AoS post-stream populations (NULL = feq(rho, u) exactly as the
+ * reference's initial `equilibrium` launch, main.cu:722-754).  N = x_count * ny.
+ * rho == NULL and u == NULL: rho = 1, u = 0 (the reference's initial values). */
+int iblb_set_state(iblb_ctx* ctx, const double* rho, const double* u, const double* f,
+                   const double* force);
+
+/* Lagrangian points for the next immersed-boundary evaluation (main.cu:834 boundary_check
+ * outputs): s [2ns] xy, u_s [2ns] xy, epsilon [ns] (NULL = all 1).  Global coordinates. */
+int iblb_set_lagrangian(iblb_ctx* ctx, int ns, const float* s, const float* u_s,
+                        const int* epsilon);
+
+/* Advance nsteps reference iterations (main.cu:852-909 each). */
+int iblb_step(iblb_ctx* ctx, int nsteps);
+
+/* Macroscopic fields after the last step as the reference holds them after `spread`:
+ * rho [N] = sum f (macro), u [2N] SoA = (sum c f + force/2)/rho.  Either may be NULL. */
+int iblb_get_macro(iblb_ctx* ctx, double* rho, double* u);
+/* Post-stream populations f^t [9N] AoS (the reference's d_f after streaming). */
+int iblb_get_populations(iblb_ctx* ctx, double* f);
+/* force^t [2N] SoA as the reference's d_force after spread (plus body_force). */
+int iblb_get_force(iblb_ctx* ctx, double* force);
+/* Lagrangian force F_s [2ns] of the last interpolation. */
+int iblb_get_lagrangian_force(iblb_ctx* ctx, float* F_s);
+/* Cumulative flux Q (ImmersedBoundary.cu:259-264).  With a multi-slab RCCL group this
+ * is the sum over all ranks; with a local group it is this slab's share. */
+int iblb_get_flux(iblb_ctx* ctx, double* Q);
+int iblb_get_step(iblb_ctx* ctx, long long* steps);
+
+/* Timing: when enabled every collide-stream launch is bracketed by HIP events on the
+ * stream it runs on; iblb_get_timing() returns the sums (and resets them if reset). */
+int iblb_set_profiling(iblb_ctx* ctx, int enabled);
+int iblb_get_timing(iblb_ctx* ctx, iblb_timing* t, int reset);
+/* The stream the context launches on (hipStream_t), for callers that add work. */
+int iblb_get_stream(iblb_ctx* ctx, void** stream);
+/* Block until all work of the context is done. */
+int iblb_synchronize(iblb_ctx* ctx);
+
+/* ---- x-slab decomposition -------------------------------------------------------
+ * Slabs are ordered along x (periodic).  A slab exchanges a one-column halo with its
+ * two neighbours every step: populations {1,5,8} of its last column go right,
+ * {3,6,7} of its first column go left.
+ *
+ * Local group: n contexts of ONE process (any devices with peer access) linked
+ * left-to-right; iblb_group_step() advances them together.  Synchronous transport,
+ * meant for testing the decomposition on one GPU.
+ *
+ * RCCL group: one context per process; rank 0 creates the id, it is broadcast by the
+ * caller (e.g. torch.distributed), every rank attaches; iblb_step() then exchanges
+ * halos with ncclSend/ncclRecv on a second stream, overlapped with the interior. */
+int iblb_link_local(iblb_ctx** ctxs, int n);
+int iblb_group_step(iblb_ctx** ctxs, int n, int nsteps);
+int iblb_rccl_unique_id(char id[IBLB_UNIQUE_ID_BYTES]);
+int iblb_attach_rccl(iblb_ctx* ctx, const char id[IBLB_UNIQUE_ID_BYTES], int nranks, int rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IBLB_H */

@@ -1,0 +1,86 @@
+"""The drop-in boundary on CPU: libiblb.so loads, exports every function include/iblb.h
+declares, and refuses to run without a HIP device (no CPU fallback)."""
+import ctypes as C
+import subprocess
+
+import numpy as np
+import pytest
+
+import cuda_iblb_11_amd as P
+from cuda_iblb_11_amd import _lib as L
+
+
+def test_library_exports_every_header_symbol():
+    names = L.header_functions()
+    assert len(names) >= 30
+    lib = L.load()
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the ctypes signature table covers exactly the header
+    assert sorted(L._SIGS) == names
+
+
+def test_exports_are_c_abi():
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    for n in L.header_functions():
+        assert n in exported, f"{n} not exported unmangled"
+
+
+def test_library_is_gfx950():
+    data = open(L.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_config_default_matches_reference_defaults():
+    cfg = L.Config()
+    assert L.load().iblb_config_default(C.byref(cfg)) == 0
+    assert (cfg.nx, cfg.ny) == (288, 192)                 # main.cu:270-271 (c_num 6 x c_space 48)
+    assert abs(cfg.tau - 2.806798146151282) < 1e-15        # main.cu:320
+    assert abs(cfg.tau2 - 0.5361251085069444) < 1e-15      # main.cu:321
+    assert cfg.flux_norm == 192.0 and cfg.flux_column == 283  # ImmersedBoundary.cu:259-261
+    assert L.load().iblb_version().decode().startswith("iblb")
+
+
+def test_create_without_device_fails_loudly():
+    if L.device_count() > 0:
+        pytest.skip("a HIP device is visible here")
+    with pytest.raises(P.IblbError) as e:
+        P.Lattice(64, 32)
+    assert e.value.code == L.IBLB_ERR_NODEVICE
+    assert "no HIP device" in str(e.value)
+
+
+def test_argument_validation_without_device():
+    lib = L.load()
+    cfg = L.Config()
+    lib.iblb_config_default(C.byref(cfg))
+    h = C.c_void_p()
+    cfg.ny = 1
+    assert lib.iblb_create(C.byref(cfg), C.byref(h)) == L.IBLB_ERR_ARG
+    cfg.ny, cfg.tau = 192, 0.4
+    assert lib.iblb_create(C.byref(cfg), C.byref(h)) == L.IBLB_ERR_ARG
+    assert lib.iblb_equilibrium(None, None, None, None, None, 4, 4, 1.0, None) == L.IBLB_ERR_ARG
+    assert lib.iblb_step(None, 1) == L.IBLB_ERR_ARG
+    assert lib.iblb_streaming(None, None, 0, 4, None) == L.IBLB_ERR_ARG
+
+
+def test_slab_plan():
+    assert P.plan_slabs(4096, 8) == [(512 * r, 512) for r in range(8)]
+    plan = P.plan_slabs(90, 4)
+    assert sum(c for _, c in plan) == 90 and plan[0][0] == 0
+    assert all(plan[i][0] + plan[i][1] == plan[i + 1][0] for i in range(3))
+    with pytest.raises(ValueError):
+        P.plan_slabs(3, 4)
+
+
+def test_split_helpers_roundtrip():
+    nx, ny = 10, 4
+    rho = np.arange(nx * ny, dtype=float)
+    parts = [P.split_state(rho, 1, nx, ny, xb, xc) for xb, xc in P.plan_slabs(nx, 3)]
+    back = np.concatenate([p.reshape(ny, -1) for p in parts], axis=1).ravel()
+    assert np.array_equal(back, rho)
+    f = np.arange(9 * nx * ny, dtype=float)
+    fp = [P.split_populations(f, nx, ny, xb, xc) for xb, xc in P.plan_slabs(nx, 2)]
+    back = np.concatenate([p.reshape(ny, -1, 9) for p in fp], axis=1).ravel()
+    assert np.array_equal(back, f)
