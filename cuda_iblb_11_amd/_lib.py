@@ -119,6 +119,13 @@ def load() -> C.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not found: build it with `make` (hipcc, gfx950); there is no CPU fallback")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 / librccl.so.1.  If torch
+    # is importable, load it first so libiblb binds to the same runtime (same SONAMEs) instead of
+    # a second copy from /opt/rocm, which would leave torch without devices.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (args, res) in _SIGS.items():
         fn = getattr(lib, name)

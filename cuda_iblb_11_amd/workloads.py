@@ -45,10 +45,13 @@ def column_state(nx: int, ny: int, seed: int = SEED, amp: float = 1e-3):
     return rho, u
 
 
-def filament(it: int, n_points: int = 256, x0: float = 1024.0, y0: float = 1.0, dy: float = 0.5,
+def filament(it: int, n_points: int = 256, x0: float = 1024.0, y0: float = 1.0, dy: float = 1.0,
              U0: float = 1e-3, period: int = 1000, sway: float = 0.0):
     """Single prescribed filament (config K3): a vertical line of points at x0 (+ sway), spacing dy,
-    velocity u_s = (U0 * (k/(n-1)) * sin(2 pi it/period), 0), epsilon = 1."""
+    velocity u_s = (U0 * (k/(n-1)) * sin(2 pi it/period), 0), epsilon = 1.
+    dy = 1 is the reference's own discretisation (96 points per 96-cell cilium, main.cu:158-170);
+    at dy = 0.5 the reference's penalty forcing (F_s = 2 delta rho (u_s - u)) over-corrects and
+    the run diverges within ~100 steps (checked with the oracle)."""
     k = np.arange(n_points, dtype=np.float64)
     ph = 2.0 * np.pi * it / period
     xs = x0 + sway * (k / max(n_points - 1, 1)) * np.sin(ph)

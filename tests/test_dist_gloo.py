@@ -43,7 +43,7 @@ def _worker(rank, world, port, nx, ny, steps, with_ib, out_dir):
     left, right = (rank - 1) % world, (rank + 1) % world
     # the same points on every rank, straddling the edge between slab 0 and slab 1
     x_edge = plan_slabs(nx, world)[0][1] - 0.6
-    pts = lambda it: W.filament(it, n_points=30, x0=x_edge, y0=2.0, dy=0.7, U0=2e-3, period=20, sway=1.5)
+    pts = lambda it: W.filament(it, n_points=30, x0=x_edge, y0=2.0, dy=1.0, U0=2e-3, period=20, sway=1.5)
     rk.collide()  # iteration 0's equilibrium + collision from rho^0, u^0, force^0
     for it in range(steps):
         send_r, send_l = rk.boundary()
@@ -89,7 +89,7 @@ def test_slab_decomposition_gloo(tmp_path, oracle, world, with_ib):
     x_edge = plan_slabs(nx, world)[0][1] - 0.6
     for it in range(steps):
         if with_ib:
-            s, us, eps = W.filament(it, n_points=30, x0=x_edge, y0=2.0, dy=0.7, U0=2e-3, period=20, sway=1.5)
+            s, us, eps = W.filament(it, n_points=30, x0=x_edge, y0=2.0, dy=1.0, U0=2e-3, period=20, sway=1.5)
             sim.set_lagrangian(s, us, eps)
         sim.step(1)
     R = np.empty((ny, nx))
