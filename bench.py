@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU sample duration")
     p.add_argument("--no-profile-events", action="store_true", help="skip per-launch HIP events")
+    p.add_argument("--same-device", action="store_true",
+                   help="testing only: every rank uses device 0 (exercise the RCCL slab path on one GPU)")
     return p.parse_args()
 
 
@@ -107,9 +109,14 @@ def main():
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
     distributed = world > 1
+    if a.same_device:
+        local = 0
     if distributed:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if a.same_device:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
 
     import cuda_iblb_11_amd as P
     from cuda_iblb_11_amd import workloads as W
@@ -143,11 +150,12 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     tm = lat.timing(reset=True)
+    red_dev = "cpu" if a.same_device else "cuda"
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        fl = torch.tensor([tm["fused_ms"] / max(tm["fused_launches"], 1)], dtype=torch.float64, device="cuda")
+        fl = torch.tensor([tm["fused_ms"] / max(tm["fused_launches"], 1)], dtype=torch.float64, device=red_dev)
         dist.all_reduce(fl, op=dist.ReduceOp.MAX)
         launch_ms = float(fl.item())
     else:
@@ -157,7 +165,7 @@ def main():
     rho_s, _ = lat.macro()
     finite = bool(np.isfinite(rho_s).all())
     if distributed:
-        fin = torch.tensor([1.0 if finite else 0.0], device="cuda")
+        fin = torch.tensor([1.0 if finite else 0.0], device=red_dev)
         dist.all_reduce(fin, op=dist.ReduceOp.MIN)
         finite = bool(fin.item() > 0)
 

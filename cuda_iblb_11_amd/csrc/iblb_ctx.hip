@@ -53,10 +53,12 @@ struct iblb_ctx {
     Layout L{};
     long fplane = 0;
     int device = 0;
+    int variant = 0;  // collide-stream kernel variant (IBLB_FUSED_VARIANT, tuning only)
     hipStream_t stream = nullptr;
     Coef coef{};
-    // populations: two buffers, `cur` holds the state
-    char* g_alloc[2] = {nullptr, nullptr};
+    // populations: two buffers in one allocation (deterministic relative placement of the
+    // 18 streams the collide-stream kernel touches), `cur` holds the state
+    char* g_alloc = nullptr;
     void* g[2] = {nullptr, nullptr};
     int cur = 0;
     // halo exchange buffers (multi-slab): 3 slots of `col` elements each, guarded
@@ -297,6 +299,7 @@ int launch_fused_step(iblb_ctx* c, int col_begin, int ncols) {
     a.flux_norm = c->cfg.flux_norm;
     a.Q = c->d_Q;
     a.c = c->coef;
+    a.variant = c->variant;
     size_t ev = 0;
     int rc = ev_begin(c, &ev);
     if (rc) return rc;
@@ -449,6 +452,9 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->nch = chunks_per_column(c->ny, c->V);
     c->device = cfg->device;
     c->max_points = cfg->max_points;
+    // collide-stream variant measured fastest on MI355X (scripts/tune_fused.py, profiles/):
+    // f64 = DPP row shift + nontemporal stores (5), f32 = nontemporal loads (2)
+    c->variant = (int)env_long("IBLB_FUSED_VARIANT", c->prec == IBLB_PREC_F64 ? 5 : 2);
     if (c->cfg.flux_column < 0) c->cfg.flux_column = c->nx - 5;
 
     const double tau = cfg->tau, tau2 = cfg->tau2, cs = 0.57735;
@@ -469,17 +475,22 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
 
     // slab layout: column stride a multiple of one wave's rows, planes padded apart
     const long col = (long)round_up((size_t)c->ny, (size_t)(64 * c->V));
-    const long pad = env_long("IBLB_PLANE_PAD", 64 * c->V);
+    // planes padded apart so the 9 read and 9 write streams do not start on the same HBM
+    // channel; a zero pad costs ~15 % (profiles/r01_tune_*.log); beyond that the choice is noise
+    const long pad = env_long("IBLB_PLANE_PAD", c->prec == IBLB_PREC_F64 ? 256 : 1024);
     c->L.ny = c->ny;
     c->L.ncol = c->ncol;
     c->L.col = col;
     c->L.plane = (long)c->ncol * col + pad;
     c->fplane = (long)c->ncol * col;
-    const size_t gbytes = (size_t)(9 * c->L.plane + 2 * GUARD) * c->esize;
-    for (int b = 0; b < 2; ++b) {
-        int rc = alloc_zero(c, (void**)&c->g_alloc[b], gbytes);
+    // buffer 1 starts `gap` elements after the end of buffer 0
+    const long gap = env_long("IBLB_BUF_GAP", c->prec == IBLB_PREC_F64 ? 320 : 0);
+    const size_t gbytes = (size_t)(2 * 9 * c->L.plane + gap + 2 * GUARD) * c->esize;
+    {
+        int rc = alloc_zero(c, (void**)&c->g_alloc, gbytes);
         if (rc) return bail(rc);
-        c->g[b] = c->g_alloc[b] + GUARD * c->esize;
+        c->g[0] = c->g_alloc + GUARD * c->esize;
+        c->g[1] = c->g_alloc + (GUARD + 9 * c->L.plane + gap) * c->esize;
     }
     // halo buffers: recv_left, recv_right, send_left, send_right; each 3 slots + guards
     {
@@ -514,8 +525,7 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    for (int b = 0; b < 2; ++b)
-        if (c->g_alloc[b]) (void)hipFree(c->g_alloc[b]);
+    if (c->g_alloc) (void)hipFree(c->g_alloc);
     void* bufs[] = {c->halo_alloc, c->rho0, c->u0, c->force0, c->d_s, c->d_us, c->d_Fs,
                     c->d_eps, c->d_nv, c->d_nv_tmp, c->fdense, c->flags, c->d_Q};
     for (void* p : bufs)

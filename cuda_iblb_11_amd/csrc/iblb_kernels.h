@@ -30,6 +30,7 @@ struct FusedArgs {
     double flux_norm;
     double* Q;
     Coef c;
+    int variant;        // kernel variant (MODE bits of lbm_kernels.hip), 0 = default
 };
 
 // Launch geometry of the collide-stream kernel: one wave per (column, 64*V-row chunk).

@@ -43,10 +43,76 @@ struct Calc<float> { typedef float R; };
 
 }  // namespace
 
+// Kernel variants (MODE bits), selected per context for A/B measurement:
+//   MODE_NT_STORE  populations written with nontemporal stores
+//   MODE_NT_LOAD   populations read with nontemporal loads (each element is read once)
+//   MODE_SHIFT     all planes loaded 16-B aligned; the +-1-row shift of the c_y != 0 planes
+//                  is done in registers (DPP wave_shr / wave_shl by one lane) with one scalar
+//                  load per wave for the element across the chunk edge, instead of
+//                  misaligned 16-B loads
+enum { MODE_NT_STORE = 1, MODE_NT_LOAD = 2, MODE_SHIFT = 4 };
+
+template <typename T, int V, int MODE>
+__device__ __forceinline__ typename VT<T, V>::type ld_plane(const T* p) {
+    typedef typename VT<T, V>::type vec;
+    if (MODE & MODE_NT_LOAD) return __builtin_nontemporal_load(reinterpret_cast<const vec*>(p));
+    return lda<T, V>(p);
+}
+template <typename T, int V, int MODE>
+__device__ __forceinline__ void st_plane(T* p, typename VT<T, V>::type v) {
+    typedef typename VT<T, V>::type vec;
+    if (MODE & MODE_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<vec*>(p));
+    else sta<T, V>(p, v);
+}
+
+// Move a 32/64-bit value one lane up (dir = +1: lane l receives lane l-1) or down
+// (dir = -1: lane l receives lane l+1) across the whole wave with DPP.
+template <int DIR>
+__device__ __forceinline__ int dpp_shift(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, DIR > 0 ? 0x138 : 0x130, 0xf, 0xf, false);
+}
+template <int DIR>
+__device__ __forceinline__ double lane_shift(double v) {
+    const int lo = dpp_shift<DIR>(__double2loint(v));
+    const int hi = dpp_shift<DIR>(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+template <int DIR>
+__device__ __forceinline__ float lane_shift(float v) {
+    return __int_as_float(dpp_shift<DIR>(__float_as_int(v)));
+}
+
+// Rows y0-1 .. y0+V-2 (DIR = +1, planes with c_y = +1) or y0+1 .. y0+V (DIR = -1) of plane
+// pointer p (column base), for a wave covering rows [cs, cs + 64V).
+template <typename T, int V, int MODE, int DIR>
+__device__ __forceinline__ typename VT<T, V>::type ld_shifted(const T* p, int y0, int cs, int lane) {
+    typedef typename VT<T, V>::type vec;
+    if (!(MODE & MODE_SHIFT)) return ldu<T, V>(p + y0 - DIR);
+    const vec a = ld_plane<T, V, MODE>(p + y0);
+    vec r;
+    if (DIR > 0) {
+        // element 0 = last element of the previous lane; lane 0: row cs-1 (scalar load)
+        T prev = lane_shift<+1>(a[V - 1]);
+        const T edge = p[cs - 1];
+        if (lane == 0) prev = edge;
+        r[0] = prev;
+#pragma unroll
+        for (int e = 1; e < V; ++e) r[e] = a[e - 1];
+    } else {
+        T next = lane_shift<-1>(a[0]);
+        const T edge = p[cs + 64 * V];
+        if (lane == 63) next = edge;
+#pragma unroll
+        for (int e = 0; e < V - 1; ++e) r[e] = a[e + 1];
+        r[V - 1] = next;
+    }
+    return r;
+}
+
 // One wave = one (column, chunk of 64*V rows); lane l owns rows y0 .. y0+V-1.
 // Column-uniform decisions (halo source, flux column, IB flag, send buffers) are
 // scalar branches.  Walls are per-lane fixes of the first / last row.
-template <typename T, int V, bool IB>
+template <typename T, int V, bool IB, int MODE>
 __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
     typedef typename VT<T, V>::type vec;
     typedef typename Calc<T>::R R;
@@ -57,7 +123,8 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
     const int xc = a.col_begin + gw / a.nch;
     const int ch = gw - (gw / a.nch) * a.nch;
     const Layout L = a.L;
-    const int y0 = ch * (64 * V) + lane * V;
+    const int cs = ch * (64 * V);
+    const int y0 = cs + lane * V;
     const long cb = (long)xc * L.col;
     const T* __restrict__ src = a.src;
 
@@ -76,16 +143,16 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
         p3 = src + 3 * L.plane + cb + L.col; p6 = src + 6 * L.plane + cb + L.col; p7 = src + 7 * L.plane + cb + L.col;
     }
 
-    // pull: cy = 0 planes aligned, cy = +1 planes from row y-1, cy = -1 planes from row y+1
-    vec v0 = lda<T, V>(p0 + y0);
-    vec v1 = lda<T, V>(p1 + y0);
-    vec v3 = lda<T, V>(p3 + y0);
-    vec v2 = ldu<T, V>(p2 + y0 - 1);
-    vec v5 = ldu<T, V>(p5 + y0 - 1);
-    vec v6 = ldu<T, V>(p6 + y0 - 1);
-    vec v4 = ldu<T, V>(p4 + y0 + 1);
-    vec v7 = ldu<T, V>(p7 + y0 + 1);
-    vec v8 = ldu<T, V>(p8 + y0 + 1);
+    // pull: c_y = 0 planes aligned, c_y = +1 planes from row y-1, c_y = -1 planes from row y+1
+    vec v0 = ld_plane<T, V, MODE>(p0 + y0);
+    vec v1 = ld_plane<T, V, MODE>(p1 + y0);
+    vec v3 = ld_plane<T, V, MODE>(p3 + y0);
+    vec v2 = ld_shifted<T, V, MODE, +1>(p2, y0, cs, lane);
+    vec v5 = ld_shifted<T, V, MODE, +1>(p5, y0, cs, lane);
+    vec v6 = ld_shifted<T, V, MODE, +1>(p6, y0, cs, lane);
+    vec v4 = ld_shifted<T, V, MODE, -1>(p4, y0, cs, lane);
+    vec v7 = ld_shifted<T, V, MODE, -1>(p7, y0, cs, lane);
+    vec v8 = ld_shifted<T, V, MODE, -1>(p8, y0, cs, lane);
     if (y0 == 0) {  // bounce-back on y = 0 (LatticeBoltzmann.cu:328-340)
         v2[0] = src[4 * L.plane + cb];
         v5[0] = src[7 * L.plane + cb];
@@ -132,15 +199,15 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
         v5[e] = (T)f[5]; v6[e] = (T)f[6]; v7[e] = (T)f[7]; v8[e] = (T)f[8];
     }
     T* dst = a.dst + cb + y0;
-    sta<T, V>(dst, v0);
-    sta<T, V>(dst + 1 * L.plane, v1);
-    sta<T, V>(dst + 2 * L.plane, v2);
-    sta<T, V>(dst + 3 * L.plane, v3);
-    sta<T, V>(dst + 4 * L.plane, v4);
-    sta<T, V>(dst + 5 * L.plane, v5);
-    sta<T, V>(dst + 6 * L.plane, v6);
-    sta<T, V>(dst + 7 * L.plane, v7);
-    sta<T, V>(dst + 8 * L.plane, v8);
+    st_plane<T, V, MODE>(dst, v0);
+    st_plane<T, V, MODE>(dst + 1 * L.plane, v1);
+    st_plane<T, V, MODE>(dst + 2 * L.plane, v2);
+    st_plane<T, V, MODE>(dst + 3 * L.plane, v3);
+    st_plane<T, V, MODE>(dst + 4 * L.plane, v4);
+    st_plane<T, V, MODE>(dst + 5 * L.plane, v5);
+    st_plane<T, V, MODE>(dst + 6 * L.plane, v6);
+    st_plane<T, V, MODE>(dst + 7 * L.plane, v7);
+    st_plane<T, V, MODE>(dst + 8 * L.plane, v8);
     if (xc == 0 && a.send_left[0]) {
         sta<T, V>(a.send_left[0] + y0, v3);
         sta<T, V>(a.send_left[1] + y0, v6);
@@ -157,17 +224,31 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
     }
 }
 
+template <typename T, int MODE>
+hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t s) {
+    constexpr int V = vec_of<T>();
+    if (a.flags)
+        fused_kernel<T, V, true, MODE><<<blocks, 256, 0, s>>>(a);
+    else
+        fused_kernel<T, V, false, MODE><<<blocks, 256, 0, s>>>(a);
+    return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s) {
-    constexpr int V = vec_of<T>();
     const long waves = (long)a.ncols * a.nch;
     if (waves <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
-    if (a.flags)
-        fused_kernel<T, V, true><<<blocks, 256, 0, s>>>(a);
-    else
-        fused_kernel<T, V, false><<<blocks, 256, 0, s>>>(a);
-    return hipGetLastError();
+    switch (a.variant) {
+        case 1: return launch_fused_mode<T, 1>(a, blocks, s);
+        case 2: return launch_fused_mode<T, 2>(a, blocks, s);
+        case 3: return launch_fused_mode<T, 3>(a, blocks, s);
+        case 4: return launch_fused_mode<T, 4>(a, blocks, s);
+        case 5: return launch_fused_mode<T, 5>(a, blocks, s);
+        case 6: return launch_fused_mode<T, 6>(a, blocks, s);
+        case 7: return launch_fused_mode<T, 7>(a, blocks, s);
+        default: return launch_fused_mode<T, 0>(a, blocks, s);
+    }
 }
 
 // ---- boot step: collide f^0 with given rho^0, u^0, force^0 (main.cu:720-754, it = 0) --

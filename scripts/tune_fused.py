@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""A/B the collide-stream kernel variants in ONE process, interleaved rounds
+(cdna_hip_programming.md §5.4 rule 24).  Each variant gets its own context (IBLB_FUSED_VARIANT
+and IBLB_PLANE_PAD are read at iblb_create); results must be bit-identical across variants.
+
+usage: tune_fused.py [--nx 4096 --ny 4096 --precision f64 --steps 100 --rounds 5]
+                     [--variants 0,1,2,...] [--pads p1,p2]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nx", type=int, default=4096)
+    ap.add_argument("--ny", type=int, default=4096)
+    ap.add_argument("--precision", default="f64")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7")
+    ap.add_argument("--pads", default="")
+    ap.add_argument("--gaps", default="", help="IBLB_BUF_GAP values, crossed with --pads")
+    a = ap.parse_args()
+    import cuda_iblb_11_amd as P
+    from cuda_iblb_11_amd import workloads as W
+    rho, u = W.perturbed_state(a.nx, a.ny, W.SEED)
+    combos = [(int(v), None, None) for v in a.variants.split(",")]
+    if a.pads:
+        gaps = [int(g) for g in a.gaps.split(",")] if a.gaps else [None]
+        combos = [(int(v), int(p), g) for v in a.variants.split(",") for p in a.pads.split(",") for g in gaps]
+    ctxs = []
+    for v, pad, gap in combos:
+        os.environ["IBLB_FUSED_VARIANT"] = str(v)
+        for name, val in (("IBLB_PLANE_PAD", pad), ("IBLB_BUF_GAP", gap)):
+            if val is None:
+                os.environ.pop(name, None)
+            else:
+                os.environ[name] = str(val)
+        lat = P.Lattice(a.nx, a.ny, W.TAU, W.TAU2, precision=a.precision, body_force=W.BODY_FORCE)
+        lat.set_state(rho, u)
+        lat.step(10)
+        lat.set_profiling(True)
+        ctxs.append(((v, pad, gap), lat))
+    for name in ("IBLB_FUSED_VARIANT", "IBLB_PLANE_PAD", "IBLB_BUF_GAP"):
+        os.environ.pop(name, None)
+    res = {k: [] for k, _ in ctxs}
+    for r in range(a.rounds):
+        for k, lat in ctxs:
+            lat.timing(reset=True)
+            lat.step(a.steps)
+            t = lat.timing(reset=True)
+            res[k].append(t["fused_ms"] / t["fused_launches"])
+        print(f"round {r} done", flush=True)
+    bpc = 18 * (8 if a.precision == "f64" else 4)
+    cells = a.nx * a.ny
+    ref_rho, ref_u = ctxs[0][1].macro()
+    for k, lat in ctxs:
+        ms = np.array(res[k])
+        r_, u_ = lat.macro()
+        same = bool(np.array_equal(r_, ref_rho) and np.array_equal(u_, ref_u))
+        row = {"variant": k[0], "pad": k[1], "gap": k[2], "median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
+               "tbps_median": bpc * cells / (np.median(ms) * 1e-3) / 1e12, "bitwise_equal_to_first": same}
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
