@@ -10,7 +10,9 @@ SRCS     := $(wildcard $(CSRC)/*.hip)
 OBJS     := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(SRCS))
 HDRS     := $(wildcard $(CSRC)/*.h) include/iblb.h
 
-all: $(LIB) oracle
+MOCK     := tests/mock_rccl/libiblb_mockrccl.so
+
+all: $(LIB) oracle $(MOCK)
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -23,8 +25,17 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -s -C oracle
 
+# test-only build: the product objects + an in-process RCCL stand-in (threads as ranks),
+# bound with -Bsymbolic so its ncclX calls never reach a real librccl in the process
+$(BUILD)/mock_rccl.o: tests/mock_rccl/mock_rccl.cpp
+	@mkdir -p $(BUILD)
+	$(HIPCC) -O2 -std=c++17 -fPIC -c $< -o $@
+
+$(MOCK): $(OBJS) $(BUILD)/mock_rccl.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-Bsymbolic -o $@ $^ -lpthread
+
 clean:
-	rm -rf $(BUILD) $(LIB)
+	rm -rf $(BUILD) $(LIB) $(MOCK)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

@@ -112,6 +112,20 @@ def header_functions() -> list[str]:
     return sorted(set(re.findall(r"\b(iblb_[a-z_]+)\s*\(", text)))
 
 
+def configure(lib: C.CDLL) -> C.CDLL:
+    """Attach the include/iblb.h signatures to a loaded library."""
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+def load_from(path: str) -> C.CDLL:
+    """Load another build of the C ABI (e.g. the mock-RCCL test build) without torch."""
+    return configure(C.CDLL(path))
+
+
 def load() -> C.CDLL:
     """Load libiblb.so (raises if it was not built; there is no fallback)."""
     global _lib
@@ -126,18 +140,13 @@ def load() -> C.CDLL:
         import torch  # noqa: F401
     except Exception:
         pass
-    lib = C.CDLL(LIB_PATH)
-    for name, (args, res) in _SIGS.items():
-        fn = getattr(lib, name)
-        fn.argtypes = args
-        fn.restype = res
-    _lib = lib
-    return lib
+    _lib = configure(C.CDLL(LIB_PATH))
+    return _lib
 
 
-def check(rc: int, ctx=None) -> None:
+def check(rc: int, ctx=None, lib: C.CDLL | None = None) -> None:
     if rc != IBLB_OK:
-        msg = load().iblb_last_error(ctx)
+        msg = (lib or load()).iblb_last_error(ctx)
         raise IblbError(rc, msg.decode() if msg else "")
 
 

@@ -96,8 +96,9 @@ class Lattice:
     def __init__(self, nx: int, ny: int, tau: float | None = None, tau2: float | None = None, *,
                  precision: str = "f64", body_force=(0.0, 0.0), flux_norm: float = 192.0,
                  flux_column: int | None = None, device: int = 0, x_begin: int = 0, x_count: int = 0,
-                 max_points: int = 0):
-        lib = L.load()
+                 max_points: int = 0, lib=None):
+        lib = lib or L.load()
+        self._lib = lib
         cfg = L.Config()
         L.check(lib.iblb_config_default(C.byref(cfg)))
         if tau is None:
@@ -115,7 +116,7 @@ class Lattice:
         cfg.max_points = int(max_points)
         h = C.c_void_p()
         rc = lib.iblb_create(C.byref(cfg), C.byref(h))
-        L.check(rc, None)
+        L.check(rc, None, lib)
         self._h = h
         self.nx, self.ny = int(nx), int(ny)
         self.x_begin = int(x_begin) if x_count > 0 else 0
@@ -128,7 +129,7 @@ class Lattice:
     # -- lifecycle ------------------------------------------------------------------------
     def close(self) -> None:
         if getattr(self, "_h", None):
-            L.load().iblb_destroy(self._h)
+            self._lib.iblb_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -144,7 +145,7 @@ class Lattice:
         self.close()
 
     def _check(self, rc: int) -> None:
-        L.check(rc, self._h)
+        L.check(rc, self._h, self._lib)
 
     @property
     def handle(self) -> C.c_void_p:
@@ -164,7 +165,7 @@ class Lattice:
         if (rho is None) != (u is None):
             rho = np.ones(self.N) if rho is None else rho
             u = np.zeros(2 * self.N) if u is None else u
-        self._check(L.load().iblb_set_state(self._h, _ptr(rho), _ptr(u), _ptr(f), _ptr(force)))
+        self._check(self._lib.iblb_set_state(self._h, _ptr(rho), _ptr(u), _ptr(f), _ptr(force)))
 
     def set_lagrangian(self, s, u_s, epsilon=None) -> None:
         s = np.ascontiguousarray(s, dtype=np.float32).ravel()
@@ -173,74 +174,75 @@ class Lattice:
         if u_s.size != 2 * ns:
             raise ValueError("s and u_s must both hold 2*Ns values")
         eps = None if epsilon is None else np.ascontiguousarray(epsilon, dtype=np.int32).ravel()
-        self._check(L.load().iblb_set_lagrangian(self._h, ns, _ptr(s), _ptr(u_s), _ptr(eps)))
+        self._check(self._lib.iblb_set_lagrangian(self._h, ns, _ptr(s), _ptr(u_s), _ptr(eps)))
         self.ns = ns
 
     def step(self, n: int = 1) -> None:
-        self._check(L.load().iblb_step(self._h, int(n)))
+        self._check(self._lib.iblb_step(self._h, int(n)))
 
     # -- readers ----------------------------------------------------------------------------
     def macro(self) -> tuple[np.ndarray, np.ndarray]:
         rho = np.empty(self.N)
         u = np.empty(2 * self.N)
-        self._check(L.load().iblb_get_macro(self._h, _ptr(rho), _ptr(u)))
+        self._check(self._lib.iblb_get_macro(self._h, _ptr(rho), _ptr(u)))
         return rho, u
 
     def populations(self) -> np.ndarray:
         f = np.empty(9 * self.N)
-        self._check(L.load().iblb_get_populations(self._h, _ptr(f)))
+        self._check(self._lib.iblb_get_populations(self._h, _ptr(f)))
         return f
 
     def force(self) -> np.ndarray:
         out = np.empty(2 * self.N)
-        self._check(L.load().iblb_get_force(self._h, _ptr(out)))
+        self._check(self._lib.iblb_get_force(self._h, _ptr(out)))
         return out
 
     def lagrangian_force(self) -> np.ndarray:
         out = np.zeros(2 * self.ns, dtype=np.float32)
-        self._check(L.load().iblb_get_lagrangian_force(self._h, _ptr(out)))
+        self._check(self._lib.iblb_get_lagrangian_force(self._h, _ptr(out)))
         return out
 
     @property
     def flux(self) -> float:
         q = C.c_double(0.0)
-        self._check(L.load().iblb_get_flux(self._h, C.byref(q)))
+        self._check(self._lib.iblb_get_flux(self._h, C.byref(q)))
         return q.value
 
     @property
     def steps(self) -> int:
         n = C.c_longlong(0)
-        self._check(L.load().iblb_get_step(self._h, C.byref(n)))
+        self._check(self._lib.iblb_get_step(self._h, C.byref(n)))
         return n.value
 
     # -- timing -----------------------------------------------------------------------------
     def set_profiling(self, on: bool = True) -> None:
-        self._check(L.load().iblb_set_profiling(self._h, 1 if on else 0))
+        self._check(self._lib.iblb_set_profiling(self._h, 1 if on else 0))
 
     def timing(self, reset: bool = False) -> dict:
         t = L.Timing()
-        self._check(L.load().iblb_get_timing(self._h, C.byref(t), 1 if reset else 0))
+        self._check(self._lib.iblb_get_timing(self._h, C.byref(t), 1 if reset else 0))
         return {k: getattr(t, k) for k, _ in L.Timing._fields_}
 
     @property
     def stream(self) -> int:
         s = C.c_void_p()
-        self._check(L.load().iblb_get_stream(self._h, C.byref(s)))
+        self._check(self._lib.iblb_get_stream(self._h, C.byref(s)))
         return s.value or 0
 
     def synchronize(self) -> None:
-        self._check(L.load().iblb_synchronize(self._h))
+        self._check(self._lib.iblb_synchronize(self._h))
 
     # -- RCCL group ---------------------------------------------------------------------------
     def attach_rccl(self, unique_id: bytes, nranks: int, rank: int) -> None:
         if len(unique_id) != L.UNIQUE_ID_BYTES:
             raise ValueError("unique id must be 128 bytes")
-        self._check(L.load().iblb_attach_rccl(self._h, unique_id, int(nranks), int(rank)))
+        self._check(self._lib.iblb_attach_rccl(self._h, unique_id, int(nranks), int(rank)))
 
 
-def rccl_unique_id() -> bytes:
+def rccl_unique_id(lib=None) -> bytes:
+    lib = lib or L.load()
     buf = C.create_string_buffer(L.UNIQUE_ID_BYTES)
-    L.check(L.load().iblb_rccl_unique_id(buf))
+    L.check(lib.iblb_rccl_unique_id(buf), None, lib)
     return buf.raw
 
 
@@ -249,17 +251,18 @@ class LocalGroup:
 
     def __init__(self, slabs: list[Lattice]):
         self.slabs = list(slabs)
+        self._lib = self.slabs[0]._lib
         self._arr = (C.c_void_p * len(self.slabs))(*[s.handle for s in self.slabs])
-        L.check(L.load().iblb_link_local(self._arr, len(self.slabs)), self.slabs[0].handle)
+        L.check(self._lib.iblb_link_local(self._arr, len(self.slabs)), self.slabs[0].handle, self._lib)
 
     def step(self, n: int = 1) -> None:
-        rc = L.load().iblb_group_step(self._arr, len(self.slabs), int(n))
+        rc = self._lib.iblb_group_step(self._arr, len(self.slabs), int(n))
         if rc != L.IBLB_OK:
             for s in self.slabs:
-                msg = L.load().iblb_last_error(s.handle)
+                msg = self._lib.iblb_last_error(s.handle)
                 if msg:
                     raise L.IblbError(rc, msg.decode())
-            L.check(rc)
+            L.check(rc, None, self._lib)
 
     def gather_macro(self) -> tuple[np.ndarray, np.ndarray]:
         """rho[N], u[2N] of the whole lattice in the reference layout."""
