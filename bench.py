@@ -160,6 +160,8 @@ def main():
         launch_ms = float(fl.item())
     else:
         launch_ms = tm["fused_ms"] / max(tm["fused_launches"], 1)
+    # cells one timed launch updates (N > 1 overlapped: the interior columns of the slab)
+    cells_per_launch = tm["fused_cells"] // max(tm["fused_launches"], 1)
 
     # sanity: the state must stay finite (macro() is collective for an RCCL group)
     rho_s, _ = lat.macro()
@@ -172,7 +174,6 @@ def main():
     cells = nx * ny
     mlups = cells * a.steps / elapsed / 1e6
     bytes_per_cell = 18 * (8 if a.precision == "f64" else 4)
-    cells_per_launch = xc * ny
     achieved = bytes_per_cell * cells_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else None
     key = f"{a.precision}_{nx}x{ny}_n{world}"
     traffic, traffic_src = pmc_traffic(key)

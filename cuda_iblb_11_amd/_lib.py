@@ -60,7 +60,7 @@ class Timing(C.Structure):
     _fields_ = [
         ("steps", C.c_longlong), ("fused_launches", C.c_longlong),
         ("fused_ms", C.c_double), ("ib_ms", C.c_double), ("halo_ms", C.c_double),
-        ("fused_bytes", C.c_double), ("cells", C.c_longlong),
+        ("fused_bytes", C.c_double), ("cells", C.c_longlong), ("fused_cells", C.c_longlong),
     ]
 
 

@@ -94,13 +94,18 @@ struct iblb_ctx {
     iblb_ctx* right = nullptr;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with the interior
+    hipEvent_t ev_bnd = nullptr;        // boundary columns + send buffers of the state written
+    hipEvent_t ev_comm = nullptr;       // halo of the state received
+    bool overlap = true;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     double fused_ms = 0., ib_ms = 0., halo_ms = 0.;
-    long long fused_launches = 0;
-    std::vector<std::pair<int, size_t>> ev_kind;  // (kind, pair index)
+    long long fused_launches = 0, fused_cells = 0;
+    struct EvRec { int kind; size_t idx; long long cells; };
+    std::vector<EvRec> ev_kind;
     std::string err;
 };
 
@@ -165,7 +170,13 @@ void send_ptrs(iblb_ctx* c, T* sl[3], T* sr[3]) {
 // ---- profiling --------------------------------------------------------------------------
 enum EvKind { EV_FUSED = 0, EV_IB = 1, EV_HALO = 2 };
 
-int ev_begin(iblb_ctx* c, size_t* idx) {
+void ev_account(iblb_ctx* c, const iblb_ctx::EvRec& r, float ms) {
+    if (r.kind == EV_FUSED) { c->fused_ms += ms; c->fused_launches++; c->fused_cells += r.cells; }
+    else if (r.kind == EV_IB) c->ib_ms += ms;
+    else c->halo_ms += ms;
+}
+
+int ev_begin(iblb_ctx* c, size_t* idx, hipStream_t st = nullptr) {
     if (!c->prof) return IBLB_OK;
     if (c->ev_used + 2 > c->ev_pool.size()) {
         for (int k = 0; k < 64; ++k) {
@@ -176,22 +187,21 @@ int ev_begin(iblb_ctx* c, size_t* idx) {
     }
     *idx = c->ev_used;
     c->ev_used += 2;
-    HIP_TRY(c, hipEventRecord(c->ev_pool[*idx], c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev_pool[*idx], st ? st : c->stream));
     return IBLB_OK;
 }
 
-int ev_end(iblb_ctx* c, size_t idx, int kind) {
+int ev_end(iblb_ctx* c, size_t idx, int kind, long long cells = 0, hipStream_t st = nullptr) {
     if (!c->prof) return IBLB_OK;
-    HIP_TRY(c, hipEventRecord(c->ev_pool[idx + 1], c->stream));
-    c->ev_kind.push_back({kind, idx});
+    HIP_TRY(c, hipEventRecord(c->ev_pool[idx + 1], st ? st : c->stream));
+    c->ev_kind.push_back({kind, idx, cells});
     if (c->ev_used >= 8192) {  // bound the pool: drain what is recorded
         HIP_TRY(c, hipEventSynchronize(c->ev_pool[idx + 1]));
-        for (auto& kv : c->ev_kind) {
+        if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));
+        for (auto& r : c->ev_kind) {
             float ms = 0.f;
-            HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_pool[kv.second], c->ev_pool[kv.second + 1]));
-            if (kv.first == EV_FUSED) { c->fused_ms += ms; c->fused_launches++; }
-            else if (kv.first == EV_IB) c->ib_ms += ms;
-            else c->halo_ms += ms;
+            HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_pool[r.idx], c->ev_pool[r.idx + 1]));
+            ev_account(c, r, ms);
         }
         c->ev_kind.clear();
         c->ev_used = 0;
@@ -200,21 +210,21 @@ int ev_end(iblb_ctx* c, size_t idx, int kind) {
 }
 
 // ---- halo exchange ----------------------------------------------------------------------
-int exchange_rccl(iblb_ctx* c) {
+int exchange_rccl(iblb_ctx* c, hipStream_t st) {
     size_t ev = 0;
-    int rc = ev_begin(c, &ev);
+    int rc = ev_begin(c, &ev, st);
     if (rc) return rc;
     const size_t n = 3 * (size_t)c->L.col;
     const ncclDataType_t dt = c->prec == IBLB_PREC_F64 ? ncclFloat64 : ncclFloat32;
     const int lr = (c->rank + c->nranks - 1) % c->nranks, rr = (c->rank + 1) % c->nranks;
     NCCL_TRY(c, ncclGroupStart());
-    NCCL_TRY(c, ncclSend(c->send_right, n, dt, rr, c->comm, c->stream));
-    NCCL_TRY(c, ncclSend(c->send_left, n, dt, lr, c->comm, c->stream));
-    NCCL_TRY(c, ncclRecv(c->recv_left, n, dt, lr, c->comm, c->stream));
-    NCCL_TRY(c, ncclRecv(c->recv_right, n, dt, rr, c->comm, c->stream));
+    NCCL_TRY(c, ncclSend(c->send_right, n, dt, rr, c->comm, st));
+    NCCL_TRY(c, ncclSend(c->send_left, n, dt, lr, c->comm, st));
+    NCCL_TRY(c, ncclRecv(c->recv_left, n, dt, lr, c->comm, st));
+    NCCL_TRY(c, ncclRecv(c->recv_right, n, dt, rr, c->comm, st));
     NCCL_TRY(c, ncclGroupEnd());
     c->halo_valid = true;
-    return ev_end(c, ev, EV_HALO);
+    return ev_end(c, ev, EV_HALO, 0, st);
 }
 
 int exchange_local(iblb_ctx* c) {
@@ -249,7 +259,7 @@ int ib_finish(iblb_ctx* c) {
 // force^t for a context that is alone or in an RCCL group (local groups: group code)
 int ensure_halo(iblb_ctx* c) {
     if (c->halo_valid || single_slab(c)) return IBLB_OK;
-    if (c->transport == TR_RCCL) return exchange_rccl(c);
+    if (c->transport == TR_RCCL) return exchange_rccl(c, c->stream);
     return fail(c, IBLB_ERR_STATE, "slab halo not available: link the slabs (iblb_link_local / iblb_attach_rccl)");
 }
 
@@ -280,7 +290,7 @@ int launch_boot_step(iblb_ctx* c) {
 }
 
 template <typename T>
-int launch_fused_step(iblb_ctx* c, int col_begin, int ncols) {
+int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, bool timed = true) {
     FusedArgs<T> a;
     a.src = gptr<T>(c, c->cur);
     a.dst = gptr<T>(c, 1 - c->cur);
@@ -288,6 +298,7 @@ int launch_fused_step(iblb_ctx* c, int col_begin, int ncols) {
     a.H = halo_of<T>(c, c->cur);
     send_ptrs<T>(c, a.send_left, a.send_right);
     a.col_begin = col_begin;
+    a.col_step = col_step;
     a.ncols = ncols;
     a.nch = c->nch;
     const bool ib = c->ib_state == IB_READY;
@@ -301,10 +312,10 @@ int launch_fused_step(iblb_ctx* c, int col_begin, int ncols) {
     a.c = c->coef;
     a.variant = c->variant;
     size_t ev = 0;
-    int rc = ev_begin(c, &ev);
+    int rc = timed ? ev_begin(c, &ev) : IBLB_OK;
     if (rc) return rc;
     HIP_TRY(c, launch_fused<T>(a, c->stream));
-    return ev_end(c, ev, EV_FUSED);
+    return timed ? ev_end(c, ev, EV_FUSED, (long long)ncols * c->ny) : IBLB_OK;
 }
 
 int free_boot(iblb_ctx* c) {
@@ -312,6 +323,31 @@ int free_boot(iblb_ctx* c) {
     if (c->u0) (void)hipFree(c->u0);
     if (c->force0) (void)hipFree(c->force0);
     c->rho0 = c->u0 = c->force0 = nullptr;
+    return IBLB_OK;
+}
+
+void after_step(iblb_ctx* c) {
+    c->cur = 1 - c->cur;
+    c->t++;
+    c->halo_valid = false;
+    c->ib_state = ib_active(c) ? IB_PENDING : IB_NONE;
+}
+
+bool rccl_multi(const iblb_ctx* c) { return c->transport == TR_RCCL && c->nranks > 1; }
+
+// RCCL slab, no IB force owed: exchange the boundary planes of the previous step on the
+// comm stream while the interior columns collide, then the two boundary columns.
+template <typename T>
+int overlapped_step(iblb_ctx* c) {
+    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+    int rc = exchange_rccl(c, c->comm_stream);
+    if (rc) return rc;
+    HIP_TRY(c, hipEventRecord(c->ev_comm, c->comm_stream));
+    if ((rc = launch_fused_step<T>(c, 1, c->ncol - 2))) return rc;
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_comm, 0));
+    if ((rc = launch_fused_step<T>(c, 0, 2, c->ncol - 1, false))) return rc;
+    HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+    after_step(c);
     return IBLB_OK;
 }
 
@@ -327,10 +363,8 @@ int advance(iblb_ctx* c) {
         rc = f64 ? launch_fused_step<double>(c, 0, c->ncol) : launch_fused_step<float>(c, 0, c->ncol);
         if (rc) return rc;
     }
-    c->cur = 1 - c->cur;
-    c->t++;
-    c->halo_valid = false;
-    c->ib_state = ib_active(c) ? IB_PENDING : IB_NONE;
+    if (rccl_multi(c)) HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+    after_step(c);
     return IBLB_OK;
 }
 
@@ -343,6 +377,9 @@ int check_ready(iblb_ctx* c) {
 
 int step_one(iblb_ctx* c) {
     int rc;
+    if (c->phase == PH_RUN && rccl_multi(c) && c->overlap && !c->halo_valid && c->ib_state != IB_PENDING &&
+        c->ncol >= 3)
+        return c->prec == IBLB_PREC_F64 ? overlapped_step<double>(c) : overlapped_step<float>(c);
     if (c->phase == PH_RUN) {
         if ((rc = ensure_halo(c))) return rc;
         if ((rc = ensure_force(c))) return rc;
@@ -523,7 +560,11 @@ void iblb_destroy(iblb_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
+    if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->g_alloc) (void)hipFree(c->g_alloc);
     void* bufs[] = {c->halo_alloc, c->rho0, c->u0, c->force0, c->d_s, c->d_us, c->d_Fs,
@@ -752,12 +793,11 @@ int iblb_get_timing(iblb_ctx* c, iblb_timing* t, int reset) {
     if (!c || !t) return IBLB_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    for (auto& kv : c->ev_kind) {
+    if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));
+    for (auto& r : c->ev_kind) {
         float ms = 0.f;
-        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_pool[kv.second], c->ev_pool[kv.second + 1]));
-        if (kv.first == EV_FUSED) { c->fused_ms += ms; c->fused_launches++; }
-        else if (kv.first == EV_IB) c->ib_ms += ms;
-        else c->halo_ms += ms;
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_pool[r.idx], c->ev_pool[r.idx + 1]));
+        ev_account(c, r, ms);
     }
     c->ev_kind.clear();
     c->ev_used = 0;
@@ -768,9 +808,10 @@ int iblb_get_timing(iblb_ctx* c, iblb_timing* t, int reset) {
     t->halo_ms = c->halo_ms;
     t->fused_bytes = 18.0 * (double)c->esize;
     t->cells = (long long)c->ncol * c->ny;
+    t->fused_cells = c->fused_cells;
     if (reset) {
         c->fused_ms = c->ib_ms = c->halo_ms = 0.;
-        c->fused_launches = 0;
+        c->fused_launches = c->fused_cells = 0;
     }
     return IBLB_OK;
 }
@@ -785,6 +826,7 @@ int iblb_synchronize(iblb_ctx* c) {
     if (!c) return IBLB_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));
     return IBLB_OK;
 }
 
@@ -925,6 +967,11 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
                 return fail(c, IBLB_ERR_ARG, "RCCL group: slabs must tile the lattice in rank order");
         }
         if (total != c->nx) return fail(c, IBLB_ERR_ARG, "RCCL group: slabs do not cover the lattice");
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
+        c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
     }
     c->halo_valid = false;
     return IBLB_OK;

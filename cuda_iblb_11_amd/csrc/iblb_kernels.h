@@ -21,6 +21,7 @@ struct FusedArgs {
     T* send_left[3];    // planes {3,6,7} of column 0 (nullptr = not sent)
     T* send_right[3];   // planes {1,5,8} of column ncol-1
     int col_begin;      // first local column handled by this launch
+    int col_step;       // distance between the columns of this launch (1 = contiguous range)
     int ncols;          // columns handled by this launch
     int nch;            // 64*V-row chunks per column
     const uint8_t* flags;  // per (column, chunk): dense IB force present (nullptr: no IB)

@@ -122,6 +122,7 @@ typedef struct iblb_timing {
     double    halo_ms;         /* summed duration of halo exchanges                      */
     double    fused_bytes;     /* algorithmic bytes per cell of the collide-stream kernel */
     long long cells;           /* cells owned by this context                            */
+    long long fused_cells;     /* lattice updates done by the timed collide-stream launches */
 } iblb_timing;
 
 /* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */
@@ -182,7 +183,9 @@ int iblb_synchronize(iblb_ctx* ctx);
  *
  * RCCL group: one context per process; rank 0 creates the id, it is broadcast by the
  * caller (e.g. torch.distributed), every rank attaches; iblb_step() then exchanges
- * halos with ncclSend/ncclRecv on a second stream, overlapped with the interior. */
+ * halos with ncclSend/ncclRecv on a second stream, overlapped with the collide of the
+ * interior columns (IBLB_OVERLAP=0 in the environment selects the sequential schedule).
+ * With an RCCL group iblb_step, iblb_set_lagrangian and every reader are collective. */
 int iblb_link_local(iblb_ctx** ctxs, int n);
 int iblb_group_step(iblb_ctx** ctxs, int n, int nsteps);
 int iblb_rccl_unique_id(char id[IBLB_UNIQUE_ID_BYTES]);

@@ -257,9 +257,10 @@ def test_errors_are_loud(gpu):
         slab.step(1)  # slab not linked to neighbours
 
 
-@pytest.mark.parametrize("n,with_ib,precision", [(2, False, "f64"), (3, False, "f64"), (2, True, "f64"),
-                                                 (4, True, "f64"), (2, False, "f32")])
-def test_rccl_slab_path_threads(gpu, n, with_ib, precision):
+@pytest.mark.parametrize("n,with_ib,precision,overlap", [(2, False, "f64", 1), (3, False, "f64", 1),
+                                                         (3, False, "f64", 0), (2, True, "f64", 1),
+                                                         (4, True, "f64", 1), (2, False, "f32", 1)])
+def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap):
     """The RCCL transport of iblb_ctx.hip (attach, halo send/recv pairing, node-value and
     flux all-reduces, collective readers) driven with N ranks as threads on the one GPU via
     the mock-RCCL test build (RCCL itself refuses two ranks on one device).  Without IB the
@@ -271,7 +272,8 @@ def test_rccl_slab_path_threads(gpu, n, with_ib, precision):
     here = os.path.dirname(os.path.abspath(__file__))
     cmd = [sys.executable, os.path.join(here, "mock_rccl", "run_group.py"), str(n), "48", "130", "25",
            "1" if with_ib else "0", precision]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, IBLB_OVERLAP=str(overlap))
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert lines, p.stdout + p.stderr
     res = json.loads(lines[-1])
