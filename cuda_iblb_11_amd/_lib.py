@@ -64,6 +64,11 @@ class Timing(C.Structure):
     ]
 
 
+class Cilia(C.Structure):
+    """struct iblb_cilia (include/iblb.h)."""
+    _fields_ = [("c_num", C.c_int), ("c_space", C.c_double), ("T", C.c_int), ("p_step", C.c_int)]
+
+
 _vp = C.c_void_p
 _SIGS = {
     # (1) reference-shaped kernels: device pointers + stream
@@ -76,6 +81,8 @@ _SIGS = {
     "iblb_spread_ex": ([_vp, _vp, _vp, C.c_int, _vp, _vp, _vp, _vp, C.c_int, C.c_int, _vp, _vp, C.c_int,
                         C.c_double, _vp], C.c_int),
     "iblb_delta": ([C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "iblb_define_filament": ([C.c_int, C.c_int, C.c_double, C.c_int, C.c_double, _vp, _vp, _vp, _vp], C.c_int),
+    "iblb_boundary_check": ([C.c_double, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
     # (2) context API
     "iblb_config_default": ([C.POINTER(Config)], C.c_int),
     "iblb_create": ([C.POINTER(Config), C.POINTER(_vp)], C.c_int),
@@ -85,6 +92,8 @@ _SIGS = {
     "iblb_device_count": ([C.POINTER(C.c_int)], C.c_int),
     "iblb_set_state": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
     "iblb_set_lagrangian": ([_vp, C.c_int, _vp, _vp, _vp], C.c_int),
+    "iblb_set_cilia": ([_vp, C.POINTER(Cilia)], C.c_int),
+    "iblb_get_lagrangian": ([_vp, _vp, _vp, _vp], C.c_int),
     "iblb_step": ([_vp, C.c_int], C.c_int),
     "iblb_get_macro": ([_vp, _vp, _vp], C.c_int),
     "iblb_get_populations": ([_vp, _vp], C.c_int),

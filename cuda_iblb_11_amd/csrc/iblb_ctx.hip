@@ -23,9 +23,14 @@
 #include <vector>
 
 #include "../../include/iblb.h"
+#include "cilia_kernels.h"
 #include "iblb_kernels.h"
 
 using namespace iblb;
+
+extern "C" {
+static int reset_cilia_state(iblb_ctx* c);
+}
 
 namespace {
 
@@ -73,6 +78,12 @@ struct iblb_ctx {
     double* force0 = nullptr;
     // immersed boundary
     int max_points = 0, ns = 0;
+    // on-device cilia kinematics (iblb_set_cilia)
+    bool cilia_on = false;
+    iblb_cilia cilia{};
+    float* cil_samples = nullptr;  // the reference's d_boundary [5 * 9600 * c_num]
+    float* cil_lasts = nullptr;    // [2 * 9600 * c_num]
+    float* cil_bpoints = nullptr;  // [5 * 96 * c_num]
     float* d_s = nullptr;
     float* d_us = nullptr;
     float* d_Fs = nullptr;
@@ -375,8 +386,28 @@ int check_ready(iblb_ctx* c) {
     return IBLB_OK;
 }
 
+// Cilia kinematics of iteration it = c->t into the Lagrangian arrays (main.cu:822-841).
+// Any force still owed to the previous points must have been evaluated before.
+int run_cilia(iblb_ctx* c) {
+    const iblb_cilia& k = c->cilia;
+    const int it = (int)c->t;
+    HIP_TRY(c, launch_define_filament(k.T, it, k.c_space, k.p_step, (double)k.c_num, c->cil_samples, c->cil_lasts,
+                                      c->cil_bpoints, c->stream));
+    HIP_TRY(c, launch_boundary_check(k.c_space, k.c_num, c->nx, it, c->cil_bpoints, c->d_s, c->d_us, c->d_eps,
+                                     c->stream));
+    c->ns = CILIA_POINTS * k.c_num;
+    return IBLB_OK;
+}
+
 int step_one(iblb_ctx* c) {
     int rc;
+    if (c->cilia_on) {
+        if (c->phase == PH_RUN) {
+            if ((rc = ensure_halo(c))) return rc;
+            if ((rc = ensure_force(c))) return rc;
+        }
+        if ((rc = run_cilia(c))) return rc;
+    }
     if (c->phase == PH_RUN && rccl_multi(c) && c->overlap && !c->halo_valid && c->ib_state != IB_PENDING &&
         c->ncol >= 3)
         return c->prec == IBLB_PREC_F64 ? overlapped_step<double>(c) : overlapped_step<float>(c);
@@ -567,7 +598,8 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->g_alloc) (void)hipFree(c->g_alloc);
-    void* bufs[] = {c->halo_alloc, c->rho0, c->u0, c->force0, c->d_s, c->d_us, c->d_Fs,
+    void* bufs[] = {c->cil_samples, c->cil_lasts, c->cil_bpoints,
+                    c->halo_alloc, c->rho0, c->u0, c->force0, c->d_s, c->d_us, c->d_Fs,
                     c->d_eps, c->d_nv, c->d_nv_tmp, c->fdense, c->flags, c->d_Q};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -630,6 +662,11 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
         HIP_TRY(c, hipMemsetAsync(c->flags, 0, (size_t)c->ncol * c->nch, c->stream));
     }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->cilia_on) {  // the beat restarts with the state (lasts = 0, main.cu:348-359)
+        int rc2 = reset_cilia_state(c);
+        if (rc2) return rc2;
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
     c->phase = PH_BOOT;
     c->t = 0;
     c->ib_state = IB_NONE;
@@ -641,6 +678,7 @@ int iblb_set_lagrangian(iblb_ctx* c, int ns, const float* s, const float* u_s, c
     if (!c || ns < 0) return IBLB_ERR_ARG;
     if (ns > c->max_points) return fail(c, IBLB_ERR_ARG, "ns exceeds max_points of the context");
     if (ns > 0 && (!s || !u_s)) return IBLB_ERR_ARG;
+    if (c->cilia_on) return fail(c, IBLB_ERR_STATE, "cilia kinematics active: points come from iblb_set_cilia");
     HIP_TRY(c, hipSetDevice(c->device));
     // force^t still owed to the old points: evaluate it before they change
     if (c->ib_state == IB_PENDING) {
@@ -661,6 +699,56 @@ int iblb_set_lagrangian(iblb_ctx* c, int ns, const float* s, const float* u_s, c
         HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
     c->ns = ns;
+    return IBLB_OK;
+}
+
+static int reset_cilia_state(iblb_ctx* c) {
+    const size_t nk = (size_t)CILIA_SAMPLES * c->cilia.c_num;
+    HIP_TRY(c, hipMemsetAsync(c->cil_samples, 0, 5 * nk * sizeof(float), c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->cil_lasts, 0, 2 * nk * sizeof(float), c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->cil_bpoints, 0, 5 * (size_t)CILIA_POINTS * c->cilia.c_num * sizeof(float),
+                              c->stream));
+    return IBLB_OK;
+}
+
+int iblb_set_cilia(iblb_ctx* c, const iblb_cilia* k) {
+    if (!c) return IBLB_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (c->ib_state == IB_PENDING) {  // force still owed to the current points
+        if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: set cilia between group steps");
+        int rc = ensure_force(c);
+        if (rc) return rc;
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (float* p : {c->cil_samples, c->cil_lasts, c->cil_bpoints})
+        if (p) (void)hipFree(p);
+    c->cil_samples = c->cil_lasts = c->cil_bpoints = nullptr;
+    c->cilia_on = false;
+    if (!k || k->c_num <= 0) return IBLB_OK;
+    if (k->T <= 0 || !(k->c_space > 0)) return fail(c, IBLB_ERR_ARG, "cilia: need T > 0 and c_space > 0");
+    if (CILIA_POINTS * k->c_num > c->max_points)
+        return fail(c, IBLB_ERR_ARG, "cilia: max_points must be >= 96 * c_num");
+    c->cilia = *k;
+    const size_t nk = (size_t)CILIA_SAMPLES * k->c_num;
+    HIP_TRY(c, hipMalloc(&c->cil_samples, 5 * nk * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&c->cil_lasts, 2 * nk * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&c->cil_bpoints, 5 * (size_t)CILIA_POINTS * k->c_num * sizeof(float)));
+    int rc = reset_cilia_state(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->cilia_on = true;
+    return IBLB_OK;
+}
+
+int iblb_get_lagrangian(iblb_ctx* c, float* s, float* u_s, int* epsilon) {
+    if (!c) return IBLB_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const size_t ns = (size_t)c->ns;
+    if (ns == 0) return IBLB_OK;
+    if (s) HIP_TRY(c, hipMemcpy(s, c->d_s, 2 * ns * sizeof(float), hipMemcpyDeviceToHost));
+    if (u_s) HIP_TRY(c, hipMemcpy(u_s, c->d_us, 2 * ns * sizeof(float), hipMemcpyDeviceToHost));
+    if (epsilon) HIP_TRY(c, hipMemcpy(epsilon, c->d_eps, ns * sizeof(int), hipMemcpyDeviceToHost));
     return IBLB_OK;
 }
 
@@ -915,6 +1003,11 @@ int iblb_group_step(iblb_ctx** cs, int n, int nsteps) {
         if (cs[0]->phase == PH_RUN) {
             if (!cs[0]->halo_valid && (rc = group_exchange(cs, n))) return rc;
             if ((rc = group_force(cs, n))) return rc;
+        }
+        for (int i = 0; i < n; ++i) {
+            if (!cs[i]->cilia_on) continue;
+            HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
+            if ((rc = run_cilia(cs[i]))) return rc;
         }
         for (int i = 0; i < n; ++i) {
             HIP_TRY(cs[i], hipSetDevice(cs[i]->device));

@@ -89,6 +89,20 @@ def spread(rho, u, f, Ns, u_s, F_s, force, s, XDIM, Q, epsilon, YDIM=None, flux_
                                float(flux_norm), _stream(stream)))
 
 
+def define_filament(T, it, c_space, p_step, c_num, s, lasts, b_points, stream=None):
+    """main.cu:77: s = d_boundary [5*9600*c_num], lasts [2*9600*c_num], b_points [5*96*c_num]."""
+    fl = _f32()
+    L.check(L.load().iblb_define_filament(int(T), int(it), float(c_space), int(p_step), float(c_num), _dev(s, fl),
+                                          _dev(lasts, fl), _dev(b_points, fl), _stream(stream)))
+
+
+def boundary_check(c_space, c_num, XDIM, it, b_points, s, u_s, epsilon, stream=None):
+    """main.cu:176: Lagrangian s [2*96*c_num], u_s, epsilon [96*c_num] from b_points."""
+    fl, i = _f32(), _i32()
+    L.check(L.load().iblb_boundary_check(float(c_space), int(c_num), int(XDIM), int(it), _dev(b_points, fl),
+                                         _dev(s, fl), _dev(u_s, fl), _dev(epsilon, i), _stream(stream)))
+
+
 def d_delta(xs, ys, x, y, out, stream=None):
     fl, i = _f32(), _i32()
     L.check(L.load().iblb_delta(int(xs.numel()), _dev(xs, fl), _dev(ys, fl), _dev(x, i), _dev(y, i), _dev(out, fl),

@@ -177,6 +177,21 @@ class Lattice:
         self._check(self._lib.iblb_set_lagrangian(self._h, ns, _ptr(s), _ptr(u_s), _ptr(eps)))
         self.ns = ns
 
+    def set_cilia(self, c_num: int, c_space: float, T: int, p_step: int) -> None:
+        """Run the reference's cilia kinematics on the device every iteration (main.cu:822-841);
+        c_num = 0 switches it off.  Needs max_points >= 96 * c_num."""
+        k = L.Cilia(int(c_num), float(c_space), int(T), int(p_step))
+        self._check(self._lib.iblb_set_cilia(self._h, C.byref(k)))
+        self.ns = 96 * int(c_num) if c_num > 0 else 0
+
+    def lagrangian(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Current Lagrangian points: s [2Ns], u_s [2Ns] (float32), epsilon [Ns] (int32)."""
+        s = np.zeros(2 * self.ns, dtype=np.float32)
+        us = np.zeros(2 * self.ns, dtype=np.float32)
+        eps = np.zeros(self.ns, dtype=np.int32)
+        self._check(self._lib.iblb_get_lagrangian(self._h, _ptr(s), _ptr(us), _ptr(eps)))
+        return s, us, eps
+
     def step(self, n: int = 1) -> None:
         self._check(self._lib.iblb_step(self._h, int(n)))
 

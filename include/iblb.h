@@ -95,6 +95,18 @@ int iblb_spread_ex(const double* rho, double* u, const double* f, int Ns, const 
 int iblb_delta(int n, const float* xs, const float* ys, const int* x, const int* y,
                float* out, void* stream);
 
+/* main.cu:77 define_filament(T, it, c_space, p_step, c_num, s, lasts, b_points): cilia beat
+ * shape, s = the reference's d_boundary [5*9600*c_num], lasts [2*9600*c_num], b_points
+ * [5*96*c_num].  Where two samples qualify for one boundary point the later one in thread
+ * order is kept (the reference leaves that race unspecified). */
+int iblb_define_filament(int T, int it, double c_space, int p_step, double c_num, float* s,
+                         float* lasts, float* b_points, void* stream);
+
+/* main.cu:176 boundary_check(c_space, c_num, XDIM, it, b_points, s, u_s, epsilon): Lagrangian
+ * points s [2*96*c_num], velocities u_s and overlap mask epsilon [96*c_num]. */
+int iblb_boundary_check(double c_space, int c_num, int XDIM, int it, const float* b_points,
+                        float* s, float* u_s, int* epsilon, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * (2) Fused context API.
  * ------------------------------------------------------------------------------- */
@@ -145,6 +157,20 @@ int iblb_set_state(iblb_ctx* ctx, const double* rho, const double* u, const doub
  * outputs): s [2ns] xy, u_s [2ns] xy, epsilon [ns] (NULL = all 1).  Global coordinates. */
 int iblb_set_lagrangian(iblb_ctx* ctx, int ns, const float* s, const float* u_s,
                         const int* epsilon);
+
+/* On-device cilia kinematics (main.cu:822-841): when set, every iblb_step iteration `it`
+ * first runs define_filament + boundary_check for `it` and uses their s, u_s, epsilon as the
+ * Lagrangian points of that iteration (no host round trip).  c_num <= 0 or NULL disables.
+ * Needs max_points >= 96 * c_num.  Excludes iblb_set_lagrangian while active. */
+typedef struct iblb_cilia {
+    int    c_num;    /* cilia (main.cu:268)                                        */
+    double c_space;  /* spacing of the cilium bases in lattice units (main.cu:280) */
+    int    T;        /* beat period in iterations (main.cu:299)                    */
+    int    p_step;   /* phase lag of neighbouring cilia, T*c_fraction/c_num (main.cu:336) */
+} iblb_cilia;
+int iblb_set_cilia(iblb_ctx* ctx, const iblb_cilia* cilia);
+/* Current Lagrangian points (the reference's d_s, d_u_s, d_epsilon; any may be NULL). */
+int iblb_get_lagrangian(iblb_ctx* ctx, float* s, float* u_s, int* epsilon);
 
 /* Advance nsteps reference iterations (main.cu:852-909 each). */
 int iblb_step(iblb_ctx* ctx, int nsteps);

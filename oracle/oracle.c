@@ -278,6 +278,112 @@ void oracle_spread_points(const double* rho, double* u, const double* f, int Ns,
     spread_finish(rho, u, f, force, XDIM, YDIM, Q, flux_column, flux_norm);
 }
 
+/* main.cu:56-74: Fourier coefficients of the beat, "WITHOUT MUCUS" set */
+static const double A_mn[7 * 2 * 3] = {
+    -0.654, 0.393, -0.097, 0.079, 0.119, 0.119, 0.009,
+    1.895, -0.018, 0.158, 0.010, 0.003, 0.013, 0.040,
+    0.787, -1.516, 0.032, -0.302, -0.252, -0.015, 0.035,
+    -0.552, -0.126, -0.341, 0.035, 0.006, -0.029, -0.068,
+    0.202, 0.716, -0.118, 0.142, 0.110, -0.013, -0.043,
+    0.096, 0.263, 0.186, -0.067, -0.032, -0.002, 0.015};
+static const double B_mn[7 * 2 * 3] = {
+    0.0, 0.284, 0.006, -0.059, 0.018, 0.053, 0.009,
+    0.0, 0.192, -0.050, 0.012, -0.007, -0.014, -0.017,
+    0.0, 1.045, 0.317, 0.226, 0.004, -0.082, -0.040,
+    0.0, -0.499, 0.423, 0.138, 0.125, 0.075, 0.067,
+    0.0, -1.017, -0.276, -0.196, -0.037, 0.025, 0.023,
+    0.0, 0.339, -0.327, -0.114, -0.105, -0.057, -0.055};
+static const double PI_REF = 3.14159; /* main.cu:29 */
+
+/* pow(float, int) of the CUDA device library, restated as float multiplications (exact
+ * for the exponents 1..3 used here: pow(a,1) = a, pow(a,2) = a*a, pow(a,3) = a*(a*a)). */
+static float pow_fi(float a, int b) {
+    float r = a;
+    for (int i = 1; i < b; i++) r = r * a;
+    return r;
+}
+
+/* main.cu:77-173, one filament sample (k, m) per reference thread, threads in order. */
+void oracle_define_filament(int T, int it, double c_space, int p_step, double c_num, float* s, float* lasts,
+                            float* b_points)
+{
+    const int f_length = 9600, length = 96;
+    const long nthreads = (long)f_length * (long)c_num;
+    for (long threadnum = 0; threadnum < nthreads; threadnum++) {
+        const int k = (int)(threadnum % f_length);
+        const int m = (int)((threadnum - k) / f_length);
+        float a_n[2 * 7], b_n[2 * 7];
+        const float arcl = (float)(1. * k / f_length);
+        int phase;
+        if (it + m * p_step == T) phase = T;
+        else phase = (it + m * p_step) % T;
+        const float offset = (float)(1. * (m - (c_num - 1) / 2.) * c_space);
+        for (int n = 0; n < 7; n++) {
+            for (int h = 0; h < 2; h++) {
+                a_n[2 * n + h] = 0.;
+                b_n[2 * n + h] = 0.;
+                for (int i = 0; i < 3; i++) {
+                    a_n[2 * n + h] = (float)(a_n[2 * n + h] + A_mn[n + 14 * i + 7 * h] * pow_fi(arcl, i + 1));
+                    b_n[2 * n + h] = (float)(b_n[2 * n + h] + B_mn[n + 14 * i + 7 * h] * pow_fi(arcl, i + 1));
+                }
+            }
+        }
+        float* sk = s + 5 * (k + (long)m * f_length);
+        sk[0] = (float)(1. * 111 * a_n[0] * 0.5 + offset);
+        sk[1] = (float)(1. * 111 * a_n[1] * 0.5);
+        sk[2] = 111 * arcl;
+        for (int n = 1; n < 7; n++) {
+            sk[0] = (float)(sk[0] + 1. * 111 * (a_n[2 * n + 0] * cos(n * 2. * PI_REF * phase / T) + b_n[2 * n + 0] * sin(n * 2. * PI_REF * phase / T)));
+            sk[1] = (float)(sk[1] + 1. * 111 * (a_n[2 * n + 1] * cos(n * 2. * PI_REF * phase / T) + b_n[2 * n + 1] * sin(n * 2. * PI_REF * phase / T)));
+        }
+        float* lk = lasts + 2 * (k + (long)m * f_length);
+        if (it > 0) {
+            sk[3] = sk[0] - lk[0];
+            sk[4] = sk[1] - lk[1];
+        }
+        lk[0] = sk[0];
+        lk[1] = sk[1];
+        for (int j = m * length; j < (m + 1) * length; j++) {
+            const float b_length = (float)(j % length);
+            if (fabsf(sk[2] - b_length) < 0.01) {
+                b_points[5 * j + 0] = sk[0];
+                b_points[5 * j + 1] = sk[1];
+                b_points[5 * j + 2] = sk[3];
+                b_points[5 * j + 3] = sk[4];
+            }
+        }
+    }
+}
+
+/* main.cu:176-252 */
+void oracle_boundary_check(double c_space, int c_num, int XDIM, int it, const float* b_points, float* s,
+                           float* u_s, int* epsilon)
+{
+    const int length = 96;
+    const int Np = length * c_num;
+    for (int j = 0; j < Np; j++) {
+        s[2 * j + 0] = (float)((c_space * c_num) / 2. + b_points[5 * j + 0]);
+        if (s[2 * j + 0] < 0) s[2 * j + 0] = s[2 * j + 0] + XDIM;
+        else if (s[2 * j + 0] > XDIM) s[2 * j + 0] = s[2 * j + 0] - XDIM;
+        s[2 * j + 1] = b_points[5 * j + 1] + 1;
+        if (it == 0) { u_s[2 * j + 0] = 0.; u_s[2 * j + 1] = 0.; }
+        else { u_s[2 * j + 0] = b_points[5 * j + 2]; u_s[2 * j + 1] = b_points[5 * j + 3]; }
+        epsilon[j] = 1;
+    }
+    const int r_max = (int)(2 * length / c_space);
+    for (int j = 0; j < Np; j++) {
+        const int m = (j - j % length) / length;
+        const float x_m = s[2 * j + 0], y_m = s[2 * j + 1];
+        for (int r = 1; r < r_max; r++)
+            for (int l = 0; l < length; l++) {
+                const int mm = (m - r < 0) ? m - r + c_num : m - r;
+                const float x_l = s[2 * (l + mm * length) + 0];
+                const float y_l = s[2 * (l + mm * length) + 1];
+                if (fabsf(x_l - x_m) < 1 && fabsf(y_l - y_m) < 1) epsilon[j] = 0;
+            }
+    }
+}
+
 /* main.cu:852-909: one iteration on f_stream. */
 void oracle_step(oracle_state* st, int it)
 {

@@ -49,6 +49,17 @@ void oracle_spread_points(const double* rho, double* u, const double* f, int Ns,
                           const float* F_s, double* force, const float* s, int XDIM, int YDIM,
                           double* Q, const int* epsilon, int flux_column, double flux_norm);
 
+/* Cilia kinematics (the reference's Lagrangian source, main.cu:56-252).
+ * define_filament: 9600 samples per cilium of the Fourier beat shape (A_mn/B_mn "without
+ * mucus", main.cu:56-74); boundary points b_points[5*96*c_num] are the samples whose arc
+ * position lies within 0.01 of an integer (main.cu:158-172; where two samples qualify, the
+ * later one in thread order is kept).  boundary_check: s, u_s and the overlap mask epsilon
+ * (main.cu:176-252; all of s is written before the mask is evaluated). */
+void oracle_define_filament(int T, int it, double c_space, int p_step, double c_num, float* s, float* lasts,
+                            float* b_points);
+void oracle_boundary_check(double c_space, int c_num, int XDIM, int it, const float* b_points, float* s,
+                           float* u_s, int* epsilon);
+
 /* One reference iteration main.cu:852-909 on host arrays:
  * equilibrium -> collision -> streaming -> macro -> [interpolate -> spread].
  * body_force (2 doubles, may be NULL) is added to force after spread (extension;

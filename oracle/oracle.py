@@ -76,6 +76,8 @@ def load(native: bool | None = None):
     for name in ("oracle_spread", "oracle_spread_points"):
         getattr(lib, name).argtypes = [_dp, _dp, _dp, C.c_int, _fp, _fp, _dp, _fp, C.c_int, C.c_int,
                                        _dp, _ip, C.c_int, C.c_double]
+    lib.oracle_define_filament.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.c_double, _fp, _fp, _fp]
+    lib.oracle_boundary_check.argtypes = [C.c_double, C.c_int, C.c_int, C.c_int, _fp, _fp, _fp, _ip]
     lib.oracle_step.argtypes = [C.POINTER(_State), C.c_int]
     lib.oracle_run.argtypes = [C.POINTER(_State), C.c_int, C.c_int]
     lib.oracle_set_threads.argtypes = [C.c_int]
@@ -119,6 +121,34 @@ def spread(rho, u, f, Ns, u_s, F_s, force, s, XDIM, Q, epsilon, YDIM=192, flux_c
     fc = XDIM - 5 if flux_column is None else flux_column
     fn = load().oracle_spread_points if point_centric else load().oracle_spread
     fn(rho, u, f, Ns, u_s, F_s, force, s, XDIM, YDIM, Q, epsilon, fc, flux_norm)
+
+
+def define_filament(T, it, c_space, p_step, c_num, s, lasts, b_points):
+    load().oracle_define_filament(int(T), int(it), float(c_space), int(p_step), float(c_num), s, lasts, b_points)
+
+
+def boundary_check(c_space, c_num, XDIM, it, b_points, s, u_s, epsilon):
+    load().oracle_boundary_check(float(c_space), int(c_num), int(XDIM), int(it), b_points, s, u_s, epsilon)
+
+
+class Cilia:
+    """The reference's Lagrangian source (main.cu:822-841) on host arrays: call points(it) once
+    per iteration, in order (define_filament keeps the previous positions in `lasts`)."""
+
+    def __init__(self, c_num, c_space, T, p_step, XDIM):
+        self.c_num, self.c_space, self.T, self.p_step, self.XDIM = int(c_num), float(c_space), int(T), int(p_step), int(XDIM)
+        nk = 9600 * self.c_num
+        self.samples = np.zeros(5 * nk, dtype=np.float32)   # d_boundary
+        self.lasts = np.zeros(2 * nk, dtype=np.float32)
+        self.b_points = np.zeros(5 * 96 * self.c_num, dtype=np.float32)
+        self.s = np.zeros(2 * 96 * self.c_num, dtype=np.float32)
+        self.u_s = np.zeros_like(self.s)
+        self.epsilon = np.ones(96 * self.c_num, dtype=np.int32)
+
+    def points(self, it):
+        define_filament(self.T, it, self.c_space, self.p_step, self.c_num, self.samples, self.lasts, self.b_points)
+        boundary_check(self.c_space, self.c_num, self.XDIM, it, self.b_points, self.s, self.u_s, self.epsilon)
+        return self.s, self.u_s, self.epsilon
 
 
 # ---- whole-step driver ----------------------------------------------------------------

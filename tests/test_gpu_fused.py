@@ -278,3 +278,31 @@ def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap):
     assert lines, p.stdout + p.stderr
     res = json.loads(lines[-1])
     assert p.returncode == 0 and res["ok"], (res, p.stderr[-2000:])
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_reference_cilia_scenario(gpu, oracle, precision):
+    """The reference's own scenario (main.cu defaults: 6 cilia, c_space 48 -> 288 x 192), with the
+    cilia kinematics running on the device inside iblb_step, against the restatement fed by the
+    restated kinematics (faster beat, T = 400, so the cilia move within the test)."""
+    from cuda_iblb_11_amd import workloads as W
+    c_num, c_space, T = 6, 48.0, 400
+    nx, ny, steps = int(c_num * c_space), 192, 40
+    p_step = T * 1 // c_num
+    sim = oracle.Simulation(nx, ny, W.TAU, W.TAU2)
+    cil = oracle.Cilia(c_num, c_space, T, p_step, nx)
+    lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, max_points=96 * c_num)
+    lat.set_state()
+    lat.set_cilia(c_num, c_space, T, p_step)
+    for it in range(steps):
+        s, us, eps = cil.points(it)
+        sim.set_lagrangian(s, us, eps)
+        sim.step(1)
+    lat.step(steps)
+    s_g, us_g, eps_g = lat.lagrangian()
+    assert np.array_equal(s_g, cil.s) and np.array_equal(us_g, cil.u_s) and np.array_equal(eps_g, cil.epsilon)
+    rho, u = lat.macro()
+    r = fields_rel(rho, u, sim.rho, sim.u, lat.N)
+    tol = 1e-9 if precision == "f64" else TOL32
+    assert max(r["rho"], r["ux"], r["uy"]) <= tol, r
+    assert abs(lat.flux - sim.flux) <= (1e-9 if precision == "f64" else 1e-3) * abs(sim.flux)

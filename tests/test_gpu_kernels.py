@@ -136,3 +136,30 @@ def test_interpolate_spread(gpu, oracle, spacing):
     assert np.max(np.abs(fg - forceo)) <= 1e-15 * np.max(np.abs(forceo))
     assert np.max(np.abs(ug - uo)) <= 1e-15 * np.max(np.abs(uo))
     assert abs(Qg[0] - Qo[0]) <= 1e-13 * abs(Qo[0])
+
+
+@pytest.mark.parametrize("c_num,c_space,T", [(6, 48.0, 1000), (12, 24.0, 300), (64, 128.0, 5000)])
+def test_cilia_kernels_bitexact(gpu, oracle, c_num, c_space, T):
+    """iblb_define_filament / iblb_boundary_check (main.cu:77, 176) against the restatement,
+    several consecutive iterations (lasts carries the previous positions)."""
+    import torch
+    from cuda_iblb_11_amd import kernels as K
+    XDIM = int(c_num * c_space)
+    p_step = T * 1 // c_num
+    cil = oracle.Cilia(c_num, c_space, T, p_step, XDIM)
+    nk = 9600 * c_num
+    samples = torch.zeros(5 * nk, dtype=torch.float32, device="cuda")
+    lasts = torch.zeros(2 * nk, dtype=torch.float32, device="cuda")
+    bp = torch.zeros(5 * 96 * c_num, dtype=torch.float32, device="cuda")
+    s = torch.zeros(2 * 96 * c_num, dtype=torch.float32, device="cuda")
+    us = torch.zeros_like(s)
+    eps = torch.zeros(96 * c_num, dtype=torch.int32, device="cuda")
+    # small beats run past it + m*p_step == T (the reference's phase = T special case)
+    iters = range(4) if c_num > 12 else range(p_step + 2)
+    for it in iters:
+        so, uso, eo = cil.points(it)
+        K.define_filament(T, it, c_space, p_step, c_num, samples, lasts, bp)
+        K.boundary_check(c_space, c_num, XDIM, it, bp, s, us, eps)
+        assert np.array_equal(_h(samples), cil.samples)
+        assert np.array_equal(_h(bp), cil.b_points)
+        assert np.array_equal(_h(s), so) and np.array_equal(_h(us), uso) and np.array_equal(_h(eps), eo)

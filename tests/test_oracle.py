@@ -168,3 +168,51 @@ def test_nominal_envelope_fixture():
     flux = np.array(d["flux"]["Q"])
     assert flux[0] == pytest.approx(-2.05717e-06)
     assert np.all(np.diff(flux[1:]) > 0)  # cumulative, monotone pumping
+
+
+def test_cilia_kinematics_kats(oracle):
+    """define_filament + boundary_check (main.cu:77-252): analytic pins of the beat.
+    * base points (arc 0) sit at x = c_space*c_num/2 + (m - (c_num-1)/2) c_space, y = 1 exactly;
+    * cilium m at iteration it has the shape of cilium 0 at it + m*p_step (metachronal lag);
+    * u_s is the per-iteration displacement of the selected sample (zero at it = 0)."""
+    c_num, c_space, T = 6, 48.0, 1000
+    p_step = T * 1 // c_num
+    cil = oracle.Cilia(c_num, c_space, T, p_step, XDIM=int(c_num * c_space))
+    s, us, eps = [a.copy() for a in cil.points(0)]
+    xy = s.reshape(c_num, 96, 2)
+    for m in range(c_num):
+        assert xy[m, 0, 1] == np.float32(1.0)
+        assert xy[m, 0, 0] == np.float32(c_space * c_num / 2 + (m - (c_num - 1) / 2) * c_space)
+    assert np.all(us == 0)
+    prev = xy.copy()
+    for it in range(1, 6):
+        s, us, eps = cil.points(it)
+        xy = s.reshape(c_num, 96, 2)
+        d = (xy - prev).reshape(-1, 2)
+        ok = np.abs(d).max(axis=1) < 1.0  # ignore points that wrapped across x = 0 / XDIM
+        assert np.allclose(us.reshape(-1, 2)[ok], d[ok], atol=6e-5)  # ulps of x ~ 288 in float
+        prev = xy.copy()
+    # lag: cilium 1 now vs cilium 0 at it + p_step
+    it = 5
+    ref = oracle.Cilia(c_num, c_space, T, p_step, XDIM=int(c_num * c_space))
+    for k in range(it + p_step + 1):
+        r, _, _ = ref.points(k)
+    a = xy[1] - [c_space, 0]
+    b = r.reshape(c_num, 96, 2)[0]
+    wrap = np.abs(a[:, 0] - b[:, 0]) > 100
+    assert np.allclose(a[~wrap], b[~wrap], atol=1e-4)
+
+
+def test_cilia_overlap_mask(oracle):
+    """Densely packed cilia (c_space 12 < 2*LENGTH/c_space range) mask points that come within one
+    lattice unit of a point of the preceding cilia; sparse cilia (c_space 128) never do."""
+    dense = oracle.Cilia(16, 12.0, 200, 200 // 16, XDIM=16 * 12)
+    masked = 0
+    for it in range(0, 200, 10):
+        _, _, eps = dense.points(it)
+        masked = max(masked, int((eps == 0).sum()))
+    assert masked > 0
+    sparse = oracle.Cilia(4, 128.0, 200, 50, XDIM=512)
+    for it in range(3):
+        _, _, eps = sparse.points(it)
+        assert np.all(eps == 1)
