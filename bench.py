@@ -34,15 +34,36 @@ sys.path.insert(0, REPO)
 METRIC = "MLUPS and achieved-HBM-GB/s, 4096² D2Q9 channel, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
+# BASELINE.json configs: (nx, ny, precision, Lagrangian points or None, description)
+WORKLOADS = {
+    "M": (4096, 4096, "f64", None, "M: 4096x4096 D2Q9 channel, no IB"),
+    "K2": (2048, 2048, "f64", None, "K2: 2048x2048 D2Q9 channel, no IB"),
+    "K3": (2048, 2048, "f64", "filament", "K3: 2048x2048 channel + one 256-point filament"),
+    "K4": (8192, 2048, "f64", None, "K4: 8192x2048 channel, no IB"),
+    "K5": (8192, 2048, "f32", "array", "K5: 8192x2048 channel + 64 filaments x 96 points"),
+}
+
+
+def workload_points(kind, nx):
+    """Static Lagrangian points (positions and velocities fixed, IB evaluated every step)."""
+    from cuda_iblb_11_amd import workloads as W
+    if kind == "filament":
+        return W.filament(250, n_points=256, x0=nx / 2 + 0.3, y0=1.0, dy=1.0, U0=1e-3, period=1000)
+    if kind == "array":
+        return W.filament_array(250, nx, n_fil=64, pts=96)
+    return None
+
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=500)
     p.add_argument("--warmup", type=int, default=50)
-    p.add_argument("--nx", type=int, default=4096)
-    p.add_argument("--ny", type=int, default=4096)
-    p.add_argument("--precision", choices=["f64", "f32"], default="f64")
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="M",
+                   help="BASELINE.json config: M (metric, default), K2..K5")
+    p.add_argument("--nx", type=int, default=None)
+    p.add_argument("--ny", type=int, default=None)
+    p.add_argument("--precision", choices=["f64", "f32"], default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU sample duration")
     p.add_argument("--no-profile-events", action="store_true", help="skip per-launch HIP events")
@@ -51,10 +72,11 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(nx, ny, budget_s):
-    """The reference's own unfused sequence (equilibrium, collision, streaming, macro, spread's
-    u correction; AoS fp64) restated in C (oracle/), OpenMP over the host cores, timed on a
-    bounded number of steps of the same workload."""
+def cpu_baseline(nx, ny, budget_s, points=None):
+    """The reference's own unfused sequence (equilibrium, collision, streaming, macro,
+    interpolate + the literal O(N*Ns) spread gather when there are points; AoS fp64) restated in
+    C (oracle/), OpenMP over the host cores, timed on a bounded number of steps of the same
+    workload."""
     from oracle import oracle as O
     from cuda_iblb_11_amd import workloads as W
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
@@ -68,8 +90,15 @@ def cpu_baseline(nx, ny, budget_s):
         O.load()
         native = False
     O.set_threads(threads)
+    ns = 0 if points is None else points[0].size // 2
+    est = nx * ny * ns * 2e-8 / threads  # ~20 ns per delta evaluation and core
+    if est > 90:
+        return {"value": None, "unit": "MLUPS", "cores": threads, "kind": kind,
+                "sample": f"skipped: the reference's O(N*Ns) spread needs ~{est:.0f} s per step on {threads} cores"}
     rho, u = W.perturbed_state(nx, ny, W.SEED)
-    sim = O.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=W.BODY_FORCE)
+    sim = O.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=W.BODY_FORCE, point_spread=False)
+    if points is not None:
+        sim.set_lagrangian(*points)
     del rho, u
     t0 = time.perf_counter()
     sim.step(1)  # warm-up + size the sample
@@ -80,7 +109,8 @@ def cpu_baseline(nx, ny, budget_s):
     dt = time.perf_counter() - t0
     mlups = nx * ny * n / dt / 1e6
     return {"value": round(mlups, 3), "unit": "MLUPS", "cores": threads, "kind": kind,
-            "sample": f"{n} steps of the {nx}x{ny} f64 channel, reference unfused AoS sequence restated in C "
+            "sample": f"{n} steps of the {nx}x{ny} f64 channel" + (f" + {ns} IB points" if ns else "") +
+                      ", reference unfused AoS sequence restated in C "
                       f"(oracle/oracle.c, {'-march=native' if native else 'x86-64-v2'}, OpenMP {threads} threads), "
                       f"{dt:.1f} s"}
 
@@ -121,10 +151,14 @@ def main():
     import cuda_iblb_11_amd as P
     from cuda_iblb_11_amd import workloads as W
 
-    nx, ny = a.nx, a.ny
+    wnx, wny, wprec, wpts, wdesc = WORKLOADS[a.workload]
+    nx, ny = a.nx or wnx, a.ny or wny
+    precision = a.precision or wprec
+    points = workload_points(wpts, nx)
+    ns = 0 if points is None else points[0].size // 2
     xb, xc = P.plan_slabs(nx, world)[rank]
-    lat = P.Lattice(nx, ny, W.TAU, W.TAU2, precision=a.precision, body_force=W.BODY_FORCE, device=local,
-                    x_begin=xb, x_count=xc if world > 1 else 0)
+    lat = P.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=W.BODY_FORCE, device=local,
+                    x_begin=xb, x_count=xc if world > 1 else 0, max_points=ns)
     rho, u = W.perturbed_state(nx, ny, W.SEED)
     lat.set_state(P.split_state(rho, 1, nx, ny, xb, xc), P.split_state(u, 2, nx, ny, xb, xc))
     del rho, u
@@ -132,6 +166,8 @@ def main():
         uid = [P.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         lat.attach_rccl(uid[0], world, rank)
+    if points is not None:
+        lat.set_lagrangian(*points)
 
     lat.step(a.warmup)
     lat.synchronize()
@@ -173,16 +209,16 @@ def main():
 
     cells = nx * ny
     mlups = cells * a.steps / elapsed / 1e6
-    bytes_per_cell = 18 * (8 if a.precision == "f64" else 4)
+    bytes_per_cell = 18 * (8 if precision == "f64" else 4)
     achieved = bytes_per_cell * cells_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else None
-    key = f"{a.precision}_{nx}x{ny}_n{world}"
+    key = f"{precision}_{nx}x{ny}_n{world}" + (f"_ib{ns}" if ns else "")
     traffic, traffic_src = pmc_traffic(key)
 
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
             lat.close()
-            cpu = cpu_baseline(nx, ny, a.cpu_seconds)
+            cpu = cpu_baseline(nx, ny, a.cpu_seconds, points)
         out = {
             "metric": METRIC,
             "value": round(mlups, 2),
@@ -194,14 +230,16 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": a.precision,
+            "dtype": precision,
             "data": "synthetic (rho = 1 + 1e-3 xi, u = 1e-3 xi, numpy seed 12345; body force 1e-6)",
             "config": {
-                "workload": f"M: {nx}x{ny} D2Q9 channel (periodic x, bounce-back y=0, mirror y=Y-1), "
-                            f"TRT+Guo, reference TAU/TAU2, no IB; one fused pull-stream+collide launch per step",
-                "nx": nx, "ny": ny, "global_cells": cells,
+                "workload": f"{wdesc} ({nx}x{ny}): D2Q9 channel (periodic x, bounce-back y=0, mirror y=Y-1), "
+                            f"TRT+Guo, reference TAU/TAU2; one fused pull-stream+collide launch per step"
+                            + (f"; IB: {ns} static Lagrangian points, interpolate+spread every step" if ns else ""),
+                "nx": nx, "ny": ny, "global_cells": cells, "ib_points": ns,
                 "parallelism": f"x-slab x{world}" + (" (RCCL halo)" if world > 1 else ""),
             },
+            "ib_ms_per_step": round(tm["ib_ms"] / a.steps, 5) if ns else None,
             "achieved_hbm_gbps": round(mlups * 1e6 * bytes_per_cell / 1e9, 1),
             "roofline": {
                 "bound": "hbm",
