@@ -282,14 +282,13 @@ def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap):
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_reference_cilia_scenario(gpu, oracle, precision):
-    """The reference's own scenario (main.cu defaults: 6 cilia, c_space 48 -> 288 x 192), with the
-    cilia kinematics running on the device inside iblb_step, against the restatement fed by the
-    restated kinematics (faster beat, T = 400, so the cilia move within the test).  The
-    reference's penalty IB diverges in this scenario after ~30 iterations, so
-    the comparison covers the first 20."""
+    """The reference's own scenario (main.cu defaults: 6 cilia, c_space 48 -> 288 x 192, T = 1e5),
+    with the cilia kinematics running on the device inside iblb_step, against the restatement
+    fed by the restated kinematics.  The reference's penalty IB diverges in this scenario after
+    ~30 iterations, so the comparison covers the first 15."""
     from cuda_iblb_11_amd import workloads as W
-    c_num, c_space, T = 6, 48.0, 400
-    nx, ny, steps = int(c_num * c_space), 192, 20
+    c_num, c_space, T = 6, 48.0, 100000
+    nx, ny, steps = int(c_num * c_space), 192, 15
     p_step = T * 1 // c_num
     sim = oracle.Simulation(nx, ny, W.TAU, W.TAU2)
     cil = oracle.Cilia(c_num, c_space, T, p_step, nx)
