@@ -3,15 +3,16 @@
 // Reference: ImmersedBoundary.cu:94-133 (interpolate), :138-267 (spread).  The
 // reference spread is a cell-centric gather over ALL points (N*Ns delta evaluations per
 // step).  The 3-point delta is zero unless |x-xs| < 1.5 and |y-ys| < 1.5, so only the
-// 3x3 nodes around (nearbyint(xs), nearbyint(ys)) receive anything; here each
-// (point, node) pair is one lane and scatters into a dense force buffer with fp64
-// atomics (9*Ns delta evaluations per step).  The per-(column, chunk) flags tell the
-// collide-stream kernel where the dense force must be read (and cleared).
+// 3x3 nodes around (nearbyint(xs), nearbyint(ys)) receive anything: each point scatters
+// into a dense force buffer with fp64 atomics (9*Ns delta evaluations per step).  The
+// per-(column, chunk) flags tell the collide-stream kernel where the dense force must be
+// read (it clears values and flag).
 //
-// Interpolation runs in two phases so that a point's nine nodes may live on different
-// slabs: ib_nodes writes (rho, u_x, u_y) of the nodes this slab owns (zeros elsewhere;
-// a sum over slabs then yields every node exactly once), ib_interp accumulates F_s in
-// the reference's node order and float rounding.
+// Single slab: one lane per point does nodes -> F_s -> spread (ib_point_kernel).  Slab
+// groups split it so a point's nine nodes may live on different slabs: ib_nodes writes
+// (rho, u_x, u_y) of the nodes this slab owns (zeros elsewhere; a sum over slabs yields
+// every node exactly once), ib_interp_spread accumulates F_s in the reference's node
+// order and float rounding and spreads into the owned columns.
 #include "iblb_kernels.h"
 
 namespace iblb {
@@ -61,10 +62,77 @@ hipError_t launch_ib_nodes(const T* g, Layout L, Halo<T> H, int nx, int x_begin,
     return hipGetLastError();
 }
 
-// ImmersedBoundary.cu:104-129: F_s accumulated in float over the nodes in c_l order,
-// each term 2*del*rho*(u_s - u) in double.
-__global__ void ib_interp_kernel(int nx, int ny, int ns, const float* __restrict__ s, const float* __restrict__ u_s,
-                                 const double* __restrict__ nv, float* __restrict__ F_s) {
+// One point, all of it: its nine nodes' rho and u_raw pulled from g (ImmersedBoundary.cu:117-128
+// via macro, LatticeBoltzmann.cu:396-405), F_s in the reference's order and float rounding, then
+// its 3x3 spread into the dense force (ImmersedBoundary.cu:189-198).  Points are independent
+// (a point's spread needs only its own F_s), so a single-slab step needs one IB launch.
+__device__ __forceinline__ void spread_point(const Layout& L, int nx, int x_begin, int x0, int y0, float xs,
+                                             float ys, float Fx, float Fy, int e, double* __restrict__ fd, long fplane,
+                                             uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
+#pragma clang fp contract(off)
+    if (e == 0) return;
+    for (int n = 0; n < 9; ++n) {
+        const int x = x0 + cx(n), y = y0 + cy(n);
+        if (x < 0 || x >= nx || y < 0 || y >= L.ny) continue;
+        const int xc = x - x_begin;
+        if (xc < 0 || xc >= L.ncol) continue;
+        const float del = d_delta(xs, ys, x, y);
+        if (del == 0.f) continue;
+        const long o = (long)xc * L.col + y;
+        atomicAdd(fd + o, (double)(Fx * del) * 1. * (double)e);
+        atomicAdd(fd + fplane + o, (double)(Fy * del) * 1. * (double)e);
+        flags[(long)xc * nch + y / rows_per_chunk] = 1;
+    }
+}
+
+template <typename T>
+__global__ void ib_point_kernel(const T* __restrict__ g, Layout L, Halo<T> H, int nx, int ns,
+                                const float* __restrict__ s, const float* __restrict__ u_s,
+                                const int* __restrict__ eps, float* __restrict__ F_s, double* __restrict__ fd,
+                                long fplane, uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
+#pragma clang fp contract(off)
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ns) return;
+    const float xs = s[2 * k + 0], ys = s[2 * k + 1];
+    const int x0 = node_x0(xs), y0 = node_x0(ys);
+    const double usx = u_s[2 * k + 0], usy = u_s[2 * k + 1];
+    float Fx = 0.f, Fy = 0.f;
+    for (int n = 0; n < 9; ++n) {
+        const int x = x0 + cx(n), y = y0 + cy(n);
+        const long j = (long)y * nx + x;
+        if (j < 0 || j >= (long)nx * L.ny) continue;
+        const int xj = (int)(j % nx), yj = (int)(j / nx);
+        double f[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) f[q] = Store<T>::to_f(pull<T>(g, L, H, xj, yj, q), q);
+        double r, mx, my;
+        moments<double>(f, r, mx, my);
+        const double del = d_delta(xs, ys, x, y);
+        Fx = (float)((double)Fx + 2. * (1. * 1. * del) * r * (usx - mx / r));
+        Fy = (float)((double)Fy + 2. * (1. * 1. * del) * r * (usy - my / r));
+    }
+    F_s[2 * k + 0] = Fx;
+    F_s[2 * k + 1] = Fy;
+    spread_point(L, nx, 0, x0, y0, xs, ys, Fx, Fy, eps ? eps[k] : 1, fd, fplane, flags, nch, rows_per_chunk);
+}
+
+template <typename T>
+hipError_t launch_ib_point(const T* g, Layout L, Halo<T> H, int nx, int ns, const float* s, const float* u_s,
+                           const int* eps, float* F_s, double* fdense, long fplane, uint8_t* flags, int nch,
+                           int rows_per_chunk, hipStream_t st) {
+    if (ns <= 0) return hipSuccess;
+    ib_point_kernel<T><<<(unsigned)((ns + 127) / 128), 128, 0, st>>>(g, L, H, nx, ns, s, u_s, eps, F_s, fdense, fplane,
+                                                                      flags, nch, rows_per_chunk);
+    return hipGetLastError();
+}
+
+// Slab groups: F_s from the node values summed over slabs, then the point's spread clipped to
+// this slab's columns.
+__global__ void ib_interp_spread_kernel(Layout L, int nx, int x_begin, int ns, const float* __restrict__ s,
+                                        const float* __restrict__ u_s, const int* __restrict__ eps,
+                                        const double* __restrict__ nv, float* __restrict__ F_s,
+                                        double* __restrict__ fd, long fplane, uint8_t* __restrict__ flags, int nch,
+                                        int rows_per_chunk) {
 #pragma clang fp contract(off)
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ns) return;
@@ -75,7 +143,7 @@ __global__ void ib_interp_kernel(int nx, int ny, int ns, const float* __restrict
     for (int n = 0; n < 9; ++n) {
         const int x = x0 + cx(n), y = y0 + cy(n);
         const long j = (long)y * nx + x;
-        if (j < 0 || j >= (long)nx * ny) continue;
+        if (j < 0 || j >= (long)nx * L.ny) continue;
         const double del = d_delta(xs, ys, x, y);
         const double* v = nv + 27L * k + 3 * n;
         Fx = (float)((double)Fx + 2. * (1. * 1. * del) * v[0] * (usx - v[1]));
@@ -83,53 +151,23 @@ __global__ void ib_interp_kernel(int nx, int ny, int ns, const float* __restrict
     }
     F_s[2 * k + 0] = Fx;
     F_s[2 * k + 1] = Fy;
+    spread_point(L, nx, x_begin, x0, y0, xs, ys, Fx, Fy, eps ? eps[k] : 1, fd, fplane, flags, nch, rows_per_chunk);
 }
 
-hipError_t launch_ib_interp(int nx, int ny, int ns, const float* s, const float* u_s, const double* node_vals,
-                            float* F_s, hipStream_t st) {
+hipError_t launch_ib_interp_spread(Layout L, int nx, int x_begin, int ns, const float* s, const float* u_s,
+                                   const int* eps, const double* node_vals, float* F_s, double* fdense, long fplane,
+                                   uint8_t* flags, int nch, int rows_per_chunk, hipStream_t st) {
     if (ns <= 0) return hipSuccess;
-    ib_interp_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(nx, ny, ns, s, u_s, node_vals, F_s);
+    ib_interp_spread_kernel<<<(unsigned)((ns + 127) / 128), 128, 0, st>>>(L, nx, x_begin, ns, s, u_s, eps, node_vals,
+                                                                          F_s, fdense, fplane, flags, nch,
+                                                                          rows_per_chunk);
     return hipGetLastError();
 }
 
-// ImmersedBoundary.cu:178-231 restated point-centrically: term = (double)(float)(F_s*del)
-// * epsilon (ImmersedBoundary.cu:196-197) added to the node's cell.  Nodes outside the
-// lattice are clipped (the reference has no periodic image in spread).
-__global__ void ib_spread_kernel(Layout L, int nx, int x_begin, int ns, const float* __restrict__ s,
-                                 const float* __restrict__ F_s, const int* __restrict__ eps,
-                                 double* __restrict__ fd, long fplane, uint8_t* __restrict__ flags, int nch,
-                                 int rows_per_chunk) {
-#pragma clang fp contract(off)
-    const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (id >= 9L * ns) return;
-    const int k = (int)(id / 9), n = (int)(id - 9L * (id / 9));
-    const int e = eps ? eps[k] : 1;
-    if (e == 0) return;
-    const float xs = s[2 * k + 0], ys = s[2 * k + 1];
-    const int x = node_x0(xs) + cx(n), y = node_x0(ys) + cy(n);
-    if (x < 0 || x >= nx || y < 0 || y >= L.ny) return;
-    const int xc = x - x_begin;
-    if (xc < 0 || xc >= L.ncol) return;
-    const float del = d_delta(xs, ys, x, y);
-    if (del == 0.f) return;
-    const double tx = (double)(F_s[2 * k + 0] * del) * 1. * (double)e;
-    const double ty = (double)(F_s[2 * k + 1] * del) * 1. * (double)e;
-    const long o = (long)xc * L.col + y;
-    atomicAdd(fd + o, tx);
-    atomicAdd(fd + fplane + o, ty);
-    flags[(long)xc * nch + y / rows_per_chunk] = 1;
-}
-
-hipError_t launch_ib_spread(Layout L, int nx, int x_begin, int ns, const float* s, const float* F_s, const int* eps,
-                            double* fdense, long fplane, uint8_t* flags, int nch, int rows_per_chunk,
-                            hipStream_t st) {
-    if (ns <= 0) return hipSuccess;
-    const long n = 9L * ns;
-    // rows_per_chunk must be the collide-stream kernel's chunk height (64*V rows)
-    ib_spread_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(L, nx, x_begin, ns, s, F_s, eps, fdense, fplane,
-                                                                  flags, nch, rows_per_chunk);
-    return hipGetLastError();
-}
+template hipError_t launch_ib_point<double>(const double*, Layout, Halo<double>, int, int, const float*, const float*,
+                                            const int*, float*, double*, long, uint8_t*, int, int, hipStream_t);
+template hipError_t launch_ib_point<float>(const float*, Layout, Halo<float>, int, int, const float*, const float*,
+                                           const int*, float*, double*, long, uint8_t*, int, int, hipStream_t);
 
 __global__ void sum_into_kernel(double* __restrict__ dst, const double* __restrict__ src, long n) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;

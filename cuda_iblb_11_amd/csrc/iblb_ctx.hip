@@ -257,12 +257,20 @@ int ib_nodes(iblb_ctx* c) {
 
 int ib_nodes_any(iblb_ctx* c) { return c->prec == IBLB_PREC_F64 ? ib_nodes<double>(c) : ib_nodes<float>(c); }
 
+// Slab groups: F_s from the summed node values, spread into this slab.  The dense force and
+// its flags are clean here: the collide that consumed the previous force cleared both.
 int ib_finish(iblb_ctx* c) {
-    const int rpc = 64 * c->V;
-    HIP_TRY(c, hipMemsetAsync(c->flags, 0, (size_t)c->ncol * c->nch, c->stream));
-    HIP_TRY(c, launch_ib_interp(c->nx, c->ny, c->ns, c->d_s, c->d_us, c->d_nv, c->d_Fs, c->stream));
-    HIP_TRY(c, launch_ib_spread(c->L, c->nx, c->x_begin, c->ns, c->d_s, c->d_Fs, c->d_eps, c->fdense, c->fplane,
-                                c->flags, c->nch, rpc, c->stream));
+    HIP_TRY(c, launch_ib_interp_spread(c->L, c->nx, c->x_begin, c->ns, c->d_s, c->d_us, c->d_eps, c->d_nv, c->d_Fs,
+                                       c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream));
+    c->ib_state = IB_READY;
+    return IBLB_OK;
+}
+
+// Single slab: the whole IB of a step in one launch.
+template <typename T>
+int ib_single(iblb_ctx* c) {
+    HIP_TRY(c, launch_ib_point<T>(gptr<T>(c, c->cur), c->L, halo_of<T>(c, c->cur), c->nx, c->ns, c->d_s, c->d_us,
+                                  c->d_eps, c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream));
     c->ib_state = IB_READY;
     return IBLB_OK;
 }
@@ -282,10 +290,13 @@ int ensure_force(iblb_ctx* c) {
     if (rc) return rc;
     size_t ev = 0;
     if ((rc = ev_begin(c, &ev))) return rc;
-    if ((rc = ib_nodes_any(c))) return rc;
-    if (c->transport == TR_RCCL && c->nranks > 1)
+    if (single_slab(c)) {
+        if ((rc = c->prec == IBLB_PREC_F64 ? ib_single<double>(c) : ib_single<float>(c))) return rc;
+    } else {
+        if ((rc = ib_nodes_any(c))) return rc;
         NCCL_TRY(c, ncclAllReduce(c->d_nv, c->d_nv, 27 * (size_t)c->ns, ncclFloat64, ncclSum, c->comm, c->stream));
-    if ((rc = ib_finish(c))) return rc;
+        if ((rc = ib_finish(c))) return rc;
+    }
     return ev_end(c, ev, EV_IB);
 }
 

@@ -24,7 +24,8 @@ struct FusedArgs {
     int col_step;       // distance between the columns of this launch (1 = contiguous range)
     int ncols;          // columns handled by this launch
     int nch;            // 64*V-row chunks per column
-    const uint8_t* flags;  // per (column, chunk): dense IB force present (nullptr: no IB)
+    uint8_t* flags;     // per (column, chunk): dense IB force present (nullptr: no IB); the
+                        // wave that consumes a chunk's force clears its values and its flag
     double* fdense;     // dense IB force, x plane then y plane (same col stride)
     long fplane;
     int flux_col;       // local column sampled for Q, or -1
@@ -74,11 +75,15 @@ hipError_t launch_field_out(const double* lay, double* ref, Layout L, int ncomp,
 template <typename T>
 hipError_t launch_ib_nodes(const T* g, Layout L, Halo<T> H, int nx, int x_begin, int ns, const float* s,
                            double* node_vals, hipStream_t st);
-hipError_t launch_ib_interp(int nx, int ny, int ns, const float* s, const float* u_s, const double* node_vals,
-                            float* F_s, hipStream_t st);
-hipError_t launch_ib_spread(Layout L, int nx, int x_begin, int ns, const float* s, const float* F_s,
-                            const int* eps, double* fdense, long fplane, uint8_t* flags, int nch,
-                            int rows_per_chunk, hipStream_t st);
 hipError_t launch_sum_into(double* dst, const double* src, long n, hipStream_t st);
+// Single slab: nodes + interpolation + spread of every point in one launch.
+template <typename T>
+hipError_t launch_ib_point(const T* g, Layout L, Halo<T> H, int nx, int ns, const float* s, const float* u_s,
+                           const int* eps, float* F_s, double* fdense, long fplane, uint8_t* flags, int nch,
+                           int rows_per_chunk, hipStream_t st);
+// Slab groups: interpolation from summed node values + spread clipped to the slab.
+hipError_t launch_ib_interp_spread(Layout L, int nx, int x_begin, int ns, const float* s, const float* u_s,
+                                   const int* eps, const double* node_vals, float* F_s, double* fdense, long fplane,
+                                   uint8_t* flags, int nch, int rows_per_chunk, hipStream_t st);
 
 }  // namespace iblb

@@ -178,6 +178,7 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
         double* fy = a.fdense + a.fplane + cb + y0;
 #pragma unroll
         for (int e = 0; e < V; ++e) { fxv[e] = fx[e]; fyv[e] = fy[e]; fx[e] = 0.; fy[e] = 0.; }
+        if (lane == 0) a.flags[(long)xc * a.nch + ch] = 0;  // only this wave reads this flag
     }
 
     const bool do_flux = xc == a.flux_col;
