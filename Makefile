@@ -11,8 +11,15 @@ OBJS     := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(SRCS))
 HDRS     := $(wildcard $(CSRC)/*.h) include/iblb.h
 
 MOCK     := tests/mock_rccl/libiblb_mockrccl.so
+# drop-in for the reference driver (main.cu; its Makefile names the binary IBLB)
+APP      := $(PKG)/bin/IBLB
+CXX      ?= g++
 
-all: $(LIB) oracle $(MOCK)
+all: $(LIB) $(APP) oracle $(MOCK)
+
+$(APP): $(PKG)/app/iblb_main.cpp include/iblb.h $(LIB)
+	@mkdir -p $(dir $(APP))
+	$(CXX) -O2 -std=c++17 -Wall -o $@ $< -L$(PKG)/lib -liblb -Wl,-rpath,'$$ORIGIN/../lib'
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -35,7 +42,7 @@ $(MOCK): $(OBJS) $(BUILD)/mock_rccl.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-Bsymbolic -o $@ $^ -lpthread
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(MOCK)
+	rm -rf $(BUILD) $(LIB) $(MOCK) $(APP)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

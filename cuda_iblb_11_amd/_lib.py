@@ -109,6 +109,9 @@ _SIGS = {
     "iblb_group_step": ([C.POINTER(_vp), C.c_int, C.c_int], C.c_int),
     "iblb_rccl_unique_id": ([C.c_char_p], C.c_int),
     "iblb_attach_rccl": ([_vp, C.c_char_p, C.c_int, C.c_int], C.c_int),
+    "iblb_gather_macro": ([_vp, C.c_int, _vp, _vp], C.c_int),
+    "iblb_save_checkpoint": ([_vp, C.c_char_p], C.c_int),
+    "iblb_load_checkpoint": ([_vp, C.c_char_p], C.c_int),
 }
 
 _lib = None

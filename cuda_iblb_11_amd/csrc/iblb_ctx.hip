@@ -105,6 +105,7 @@ struct iblb_ctx {
     iblb_ctx* right = nullptr;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    std::vector<int> slab_begin, slab_count;  // every rank's columns (RCCL group)
     hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with the interior
     hipEvent_t ev_bnd = nullptr;        // boundary columns + send buffers of the state written
     hipEvent_t ev_comm = nullptr;       // halo of the state received
@@ -149,6 +150,7 @@ template <typename T>
 T* gptr(iblb_ctx* c, int which) { return (T*)c->g[which]; }
 
 bool single_slab(const iblb_ctx* c) { return c->ncol == c->nx && c->transport != TR_LOCAL && c->nranks <= 1; }
+bool rccl_multi(const iblb_ctx* c) { return c->transport == TR_RCCL && c->nranks > 1; }
 bool ib_active(const iblb_ctx* c) { return c->max_points > 0 && c->ns > 0; }
 
 template <typename T>
@@ -244,6 +246,23 @@ int exchange_local(iblb_ctx* c) {
     HIP_TRY(c, hipMemcpyAsync(c->recv_left, c->left->send_right, bytes, hipMemcpyDefault, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->recv_right, c->right->send_left, bytes, hipMemcpyDefault, c->stream));
     c->halo_valid = true;
+    return IBLB_OK;
+}
+
+// send buffers of the state in g[cur] (normally written by the collide that produced it)
+int pack_send(iblb_ctx* c) {
+    if (c->phase != PH_RUN || single_slab(c) || c->transport == TR_NONE) return IBLB_OK;
+    const size_t n = (size_t)c->ny * c->esize;
+    char* g = (char*)c->g[c->cur];
+    for (int p = 0; p < 3; ++p) {
+        const char* r = g + ((size_t)left_plane(p) * c->L.plane + (size_t)(c->ncol - 1) * c->L.col) * c->esize;
+        const char* l = g + (size_t)right_plane(p) * c->L.plane * c->esize;
+        HIP_TRY(c, hipMemcpyAsync((char*)c->send_right + p * c->L.col * c->esize, r, n, hipMemcpyDeviceToDevice,
+                                  c->stream));
+        HIP_TRY(c, hipMemcpyAsync((char*)c->send_left + p * c->L.col * c->esize, l, n, hipMemcpyDeviceToDevice,
+                                  c->stream));
+    }
+    if (rccl_multi(c)) HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
     return IBLB_OK;
 }
 
@@ -355,8 +374,6 @@ void after_step(iblb_ctx* c) {
     c->ib_state = ib_active(c) ? IB_PENDING : IB_NONE;
 }
 
-bool rccl_multi(const iblb_ctx* c) { return c->transport == TR_RCCL && c->nranks > 1; }
-
 // RCCL slab, no IB force owed: exchange the boundary planes of the previous step on the
 // comm stream while the interior columns collide, then the two boundary columns.
 template <typename T>
@@ -463,6 +480,24 @@ int prepare_read(iblb_ctx* c) {
     }
     if ((rc = ensure_halo(c))) return rc;
     return ensure_force(c);
+}
+
+// rho [N] and u [2N] of the slab in the reference layout (j = y*ncol + xc), into device
+// buffers, on the context's stream.  The state must be prepared (prepare_read).
+int macro_device(iblb_ctx* c, double* dr, double* du) {
+    if (c->phase == PH_BOOT) {
+        HIP_TRY(c, launch_field_out(c->rho0, dr, c->L, 1, c->fplane, 0., 0., c->stream));
+        HIP_TRY(c, launch_field_out(c->u0, du, c->L, 2, c->fplane, 0., 0., c->stream));
+        return IBLB_OK;
+    }
+    const double* fd = c->ib_state == IB_READY ? c->fdense : nullptr;
+    if (c->prec == IBLB_PREC_F64)
+        HIP_TRY(c, launch_macro_out<double>(gptr<double>(c, c->cur), c->L, halo_of<double>(c, c->cur), fd, c->fplane,
+                                            c->coef.gx, c->coef.gy, dr, du, c->stream));
+    else
+        HIP_TRY(c, launch_macro_out<float>(gptr<float>(c, c->cur), c->L, halo_of<float>(c, c->cur), fd, c->fplane,
+                                           c->coef.gx, c->coef.gy, dr, du, c->stream));
+    return IBLB_OK;
 }
 
 }  // namespace
@@ -782,24 +817,12 @@ int iblb_get_macro(iblb_ctx* c, double* rho, double* u) {
     HIP_TRY(c, hipSetDevice(c->device));
     const long N = (long)c->ncol * c->ny;
     const size_t nb = (size_t)N * sizeof(double);
-    DevBuf dr, du;
-    HIP_TRY(c, hipMalloc(&dr.p, nb));
-    HIP_TRY(c, hipMalloc(&du.p, 2 * nb));
-    if (c->phase == PH_BOOT) {
-        HIP_TRY(c, launch_field_out(c->rho0, (double*)dr.p, c->L, 1, c->fplane, 0., 0., c->stream));
-        HIP_TRY(c, launch_field_out(c->u0, (double*)du.p, c->L, 2, c->fplane, 0., 0., c->stream));
-    } else {
-        const double* fd = c->ib_state == IB_READY ? c->fdense : nullptr;
-        if (c->prec == IBLB_PREC_F64)
-            HIP_TRY(c, launch_macro_out<double>(gptr<double>(c, c->cur), c->L, halo_of<double>(c, c->cur), fd, c->fplane,
-                                                c->coef.gx, c->coef.gy, (double*)dr.p, (double*)du.p, c->stream));
-        else
-            HIP_TRY(c, launch_macro_out<float>(gptr<float>(c, c->cur), c->L, halo_of<float>(c, c->cur), fd, c->fplane,
-                                               c->coef.gx, c->coef.gy, (double*)dr.p, (double*)du.p, c->stream));
-    }
+    DevBuf d;
+    HIP_TRY(c, hipMalloc(&d.p, 3 * nb));
+    if ((rc = macro_device(c, (double*)d.p, (double*)d.p + N))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (rho) HIP_TRY(c, hipMemcpy(rho, dr.p, nb, hipMemcpyDeviceToHost));
-    if (u) HIP_TRY(c, hipMemcpy(u, du.p, 2 * nb, hipMemcpyDeviceToHost));
+    if (rho) HIP_TRY(c, hipMemcpy(rho, d.p, nb, hipMemcpyDeviceToHost));
+    if (u) HIP_TRY(c, hipMemcpy(u, (double*)d.p + N, 2 * nb, hipMemcpyDeviceToHost));
     return IBLB_OK;
 }
 
@@ -930,6 +953,14 @@ int iblb_synchronize(iblb_ctx* c) {
 }
 
 // ---- local groups ---------------------------------------------------------------------------
+static int sync_all(iblb_ctx** cs, int n) {
+    for (int i = 0; i < n; ++i) {
+        HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
+        HIP_TRY(cs[i], hipStreamSynchronize(cs[i]->stream));
+    }
+    return IBLB_OK;
+}
+
 int iblb_link_local(iblb_ctx** ctxs, int n) {
     if (!ctxs || n < 1) return IBLB_ERR_ARG;
     for (int i = 0; i < n; ++i) {
@@ -950,16 +981,11 @@ int iblb_link_local(iblb_ctx** ctxs, int n) {
         ctxs[i]->left = ctxs[(i + n - 1) % n];
         ctxs[i]->right = ctxs[(i + 1) % n];
         ctxs[i]->halo_valid = false;
+        HIP_TRY(ctxs[i], hipSetDevice(ctxs[i]->device));
+        int rc = pack_send(ctxs[i]);  // a restored state has no send buffers yet
+        if (rc) return rc;
     }
-    return IBLB_OK;
-}
-
-static int sync_all(iblb_ctx** cs, int n) {
-    for (int i = 0; i < n; ++i) {
-        HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
-        HIP_TRY(cs[i], hipStreamSynchronize(cs[i]->stream));
-    }
-    return IBLB_OK;
+    return sync_all(ctxs, n);
 }
 
 static int group_exchange(iblb_ctx** cs, int n) {
@@ -1071,6 +1097,12 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
                 return fail(c, IBLB_ERR_ARG, "RCCL group: slabs must tile the lattice in rank order");
         }
         if (total != c->nx) return fail(c, IBLB_ERR_ARG, "RCCL group: slabs do not cover the lattice");
+        c->slab_begin.resize(nranks);
+        c->slab_count.resize(nranks);
+        for (int r = 0; r < nranks; ++r) {
+            c->slab_begin[r] = all[2 * r];
+            c->slab_count[r] = all[2 * r + 1];
+        }
         HIP_TRY(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
@@ -1078,6 +1110,205 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
     }
     c->halo_valid = false;
+    int rc = pack_send(c);  // a restored state has no send buffers yet
+    if (rc) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return IBLB_OK;
+}
+
+// ---- output gather (RCCL group) -----------------------------------------------------------
+int iblb_gather_macro(iblb_ctx* c, int root, double* rho, double* u) {
+    if (!c) return IBLB_ERR_ARG;
+    if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: gather the slabs' iblb_get_macro");
+    if (!rccl_multi(c)) return iblb_get_macro(c, rho, u);
+    if (root < 0 || root >= c->nranks) return fail(c, IBLB_ERR_ARG, "root rank out of range");
+    int rc = prepare_read(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const long N = (long)c->ncol * c->ny;
+    DevBuf mine, all;
+    HIP_TRY(c, hipMalloc(&mine.p, 3 * (size_t)N * sizeof(double)));
+    if ((rc = macro_device(c, (double*)mine.p, (double*)mine.p + N))) return rc;
+    const bool is_root = c->rank == root;
+    const size_t total = 3 * (size_t)c->nx * c->ny;
+    if (is_root) HIP_TRY(c, hipMalloc(&all.p, total * sizeof(double)));
+    // rank r's [rho | u] block lands at 3*ny*x_begin_r in rank order
+    NCCL_TRY(c, ncclGroupStart());
+    if (is_root) {
+        for (int r = 0; r < c->nranks; ++r) {
+            double* dst = (double*)all.p + 3L * c->ny * c->slab_begin[r];
+            const size_t n = 3 * (size_t)c->ny * c->slab_count[r];
+            if (r == root)
+                HIP_TRY(c, hipMemcpyAsync(dst, mine.p, n * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+            else
+                NCCL_TRY(c, ncclRecv(dst, n, ncclFloat64, r, c->comm, c->stream));
+        }
+    } else {
+        NCCL_TRY(c, ncclSend(mine.p, 3 * (size_t)N, ncclFloat64, root, c->comm, c->stream));
+    }
+    NCCL_TRY(c, ncclGroupEnd());
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (!is_root || (!rho && !u)) return IBLB_OK;
+    std::vector<double> h(total);
+    HIP_TRY(c, hipMemcpy(h.data(), all.p, total * sizeof(double), hipMemcpyDeviceToHost));
+    const long nx = c->nx, ny = c->ny, G = nx * ny;
+    for (int r = 0; r < c->nranks; ++r) {
+        const long xb = c->slab_begin[r], nc = c->slab_count[r], n = nc * ny;
+        const double* blk = h.data() + 3 * ny * xb;
+        for (long y = 0; y < ny; ++y)
+            for (long xc = 0; xc < nc; ++xc) {
+                const long j = y * nc + xc, g = y * nx + xb + xc;
+                if (rho) rho[g] = blk[j];
+                if (u) {
+                    u[g] = blk[n + j];
+                    u[G + g] = blk[2 * n + j];
+                }
+            }
+    }
+    return IBLB_OK;
+}
+
+// ---- checkpoint / restart ---------------------------------------------------------------------
+// File: 8-byte magic, 12 int64 fields, 6 doubles, then the stored populations g (plane i, column
+// xc, rows y; storage precision, no padding), the Lagrangian points and the cilia buffers.
+namespace {
+const char CKPT_MAGIC[8] = {'I', 'B', 'L', 'B', 'C', 'K', '0', '1'};
+enum { CK_VERSION, CK_NX, CK_NY, CK_XB, CK_NCOL, CK_PREC, CK_T, CK_NS, CK_CILIA, CK_CNUM, CK_CT, CK_CPSTEP, CK_NI };
+enum { CK_Q, CK_CSPACE, CK_TAU, CK_TAU2, CK_GX, CK_GY, CK_ND };
+
+struct File {
+    FILE* f = nullptr;
+    ~File() { if (f) std::fclose(f); }
+};
+
+int ck_io(iblb_ctx* c, bool ok) { return ok ? IBLB_OK : fail(c, IBLB_ERR_ARG, "checkpoint file truncated or unwritable"); }
+
+// device <-> file through a host bounce buffer
+int ck_dev(iblb_ctx* c, File& fl, bool save, void* dev, size_t bytes) {
+    if (bytes == 0) return IBLB_OK;
+    std::vector<char> h(bytes);
+    if (save) {
+        HIP_TRY(c, hipMemcpy(h.data(), dev, bytes, hipMemcpyDeviceToHost));
+        return ck_io(c, std::fwrite(h.data(), 1, bytes, fl.f) == bytes);
+    }
+    if (std::fread(h.data(), 1, bytes, fl.f) != bytes) return ck_io(c, false);
+    HIP_TRY(c, hipMemcpy(dev, h.data(), bytes, hipMemcpyHostToDevice));
+    return IBLB_OK;
+}
+
+int ck_pops(iblb_ctx* c, File& fl, bool save) {
+    const size_t w = (size_t)c->ny * c->esize, pitch = (size_t)c->L.col * c->esize;
+    std::vector<char> h(w * c->ncol);
+    for (int i = 0; i < 9; ++i) {
+        char* plane = (char*)c->g[c->cur] + (size_t)i * c->L.plane * c->esize;
+        if (save) {
+            HIP_TRY(c, hipMemcpy2D(h.data(), w, plane, pitch, w, c->ncol, hipMemcpyDeviceToHost));
+            if (std::fwrite(h.data(), 1, h.size(), fl.f) != h.size()) return ck_io(c, false);
+        } else {
+            if (std::fread(h.data(), 1, h.size(), fl.f) != h.size()) return ck_io(c, false);
+            HIP_TRY(c, hipMemcpy2D(plane, pitch, h.data(), w, w, c->ncol, hipMemcpyHostToDevice));
+        }
+    }
+    return IBLB_OK;
+}
+
+}  // namespace
+
+int iblb_save_checkpoint(iblb_ctx* c, const char* path) {
+    if (!c || !path) return IBLB_ERR_ARG;
+    if (c->phase != PH_RUN) return fail(c, IBLB_ERR_STATE, "checkpoint needs a state advanced by at least one step");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));
+    File fl;
+    const std::string tmp = std::string(path) + ".tmp";
+    fl.f = std::fopen(tmp.c_str(), "wb");
+    if (!fl.f) return fail(c, IBLB_ERR_ARG, std::string("cannot open ") + tmp + " for writing");
+    double Q = 0.;
+    HIP_TRY(c, hipMemcpy(&Q, c->d_Q, sizeof(double), hipMemcpyDeviceToHost));
+    long long iv[CK_NI] = {1, c->nx, c->ny, c->x_begin, c->ncol, c->prec, c->t, c->ns, c->cilia_on ? 1 : 0,
+                           c->cilia.c_num, c->cilia.T, c->cilia.p_step};
+    double dv[CK_ND] = {Q, c->cilia.c_space, c->cfg.tau, c->cfg.tau2, c->coef.gx, c->coef.gy};
+    int rc = ck_io(c, std::fwrite(CKPT_MAGIC, 1, 8, fl.f) == 8 && std::fwrite(iv, sizeof(iv), 1, fl.f) == 1 &&
+                          std::fwrite(dv, sizeof(dv), 1, fl.f) == 1);
+    if (rc || (rc = ck_pops(c, fl, true))) return rc;
+    const size_t ns = (size_t)c->ns;
+    if ((rc = ck_dev(c, fl, true, c->d_s, 2 * ns * sizeof(float))) ||
+        (rc = ck_dev(c, fl, true, c->d_us, 2 * ns * sizeof(float))) ||
+        (rc = ck_dev(c, fl, true, c->d_eps, ns * sizeof(int))))
+        return rc;
+    if (c->cilia_on) {
+        const size_t nk = (size_t)CILIA_SAMPLES * c->cilia.c_num;
+        if ((rc = ck_dev(c, fl, true, c->cil_samples, 5 * nk * sizeof(float))) ||
+            (rc = ck_dev(c, fl, true, c->cil_lasts, 2 * nk * sizeof(float))) ||
+            (rc = ck_dev(c, fl, true, c->cil_bpoints, 5 * (size_t)CILIA_POINTS * c->cilia.c_num * sizeof(float))))
+            return rc;
+    }
+    const bool ok = std::fflush(fl.f) == 0;
+    std::fclose(fl.f);
+    fl.f = nullptr;
+    if (!ok || std::rename(tmp.c_str(), path) != 0) return fail(c, IBLB_ERR_ARG, std::string("cannot write ") + path);
+    return IBLB_OK;
+}
+
+int iblb_load_checkpoint(iblb_ctx* c, const char* path) {
+    if (!c || !path) return IBLB_ERR_ARG;
+    if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: restore the slabs before linking");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    File fl;
+    fl.f = std::fopen(path, "rb");
+    if (!fl.f) return fail(c, IBLB_ERR_ARG, std::string("cannot open ") + path);
+    char magic[8];
+    long long iv[CK_NI];
+    double dv[CK_ND];
+    if (std::fread(magic, 1, 8, fl.f) != 8 || std::memcmp(magic, CKPT_MAGIC, 8) != 0)
+        return fail(c, IBLB_ERR_ARG, "not an iblb checkpoint");
+    if (std::fread(iv, sizeof(iv), 1, fl.f) != 1 || std::fread(dv, sizeof(dv), 1, fl.f) != 1) return ck_io(c, false);
+    if (iv[CK_VERSION] != 1) return fail(c, IBLB_ERR_ARG, "unsupported checkpoint version");
+    if (iv[CK_NX] != c->nx || iv[CK_NY] != c->ny || iv[CK_XB] != c->x_begin || iv[CK_NCOL] != c->ncol ||
+        iv[CK_PREC] != c->prec)
+        return fail(c, IBLB_ERR_ARG, "checkpoint lattice/slab/precision differs from the context");
+    if (dv[CK_TAU] != c->cfg.tau || dv[CK_TAU2] != c->cfg.tau2 || dv[CK_GX] != c->coef.gx || dv[CK_GY] != c->coef.gy)
+        return fail(c, IBLB_ERR_ARG, "checkpoint relaxation times / body force differ from the context");
+    if (iv[CK_NS] > c->max_points) return fail(c, IBLB_ERR_ARG, "checkpoint holds more points than max_points");
+    int rc;
+    // cilia configuration first (allocates its buffers), then every array
+    if (iv[CK_CILIA]) {
+        iblb_cilia k{(int)iv[CK_CNUM], dv[CK_CSPACE], (int)iv[CK_CT], (int)iv[CK_CPSTEP]};
+        c->ib_state = IB_NONE;
+        if ((rc = iblb_set_cilia(c, &k))) return rc;
+    } else if (c->cilia_on) {
+        c->ib_state = IB_NONE;
+        if ((rc = iblb_set_cilia(c, nullptr))) return rc;
+    }
+    if ((rc = ck_pops(c, fl, false))) return rc;
+    const size_t ns = (size_t)iv[CK_NS];
+    if ((rc = ck_dev(c, fl, false, c->d_s, 2 * ns * sizeof(float))) ||
+        (rc = ck_dev(c, fl, false, c->d_us, 2 * ns * sizeof(float))) ||
+        (rc = ck_dev(c, fl, false, c->d_eps, ns * sizeof(int))))
+        return rc;
+    if (c->cilia_on) {
+        const size_t nk = (size_t)CILIA_SAMPLES * c->cilia.c_num;
+        if ((rc = ck_dev(c, fl, false, c->cil_samples, 5 * nk * sizeof(float))) ||
+            (rc = ck_dev(c, fl, false, c->cil_lasts, 2 * nk * sizeof(float))) ||
+            (rc = ck_dev(c, fl, false, c->cil_bpoints, 5 * (size_t)CILIA_POINTS * c->cilia.c_num * sizeof(float))))
+            return rc;
+    }
+    free_boot(c);
+    double q[4] = {dv[CK_Q], 0., 0., 0.};
+    HIP_TRY(c, hipMemcpy(c->d_Q, q, sizeof(q), hipMemcpyHostToDevice));
+    if (c->fdense) {
+        HIP_TRY(c, hipMemsetAsync(c->fdense, 0, 2 * (size_t)c->fplane * sizeof(double), c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->flags, 0, (size_t)c->ncol * c->nch, c->stream));
+    }
+    c->ns = (int)ns;
+    c->t = iv[CK_T];
+    c->phase = PH_RUN;
+    c->halo_valid = false;
+    c->ib_state = ib_active(c) ? IB_PENDING : IB_NONE;  // force^t is re-evaluated from g and the points
+    if ((rc = pack_send(c))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     return IBLB_OK;
 }
 

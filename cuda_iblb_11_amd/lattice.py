@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -247,11 +248,27 @@ class Lattice:
     def synchronize(self) -> None:
         self._check(self._lib.iblb_synchronize(self._h))
 
+    # -- checkpoint / restart -------------------------------------------------------------------
+    def save_checkpoint(self, path) -> None:
+        self._check(self._lib.iblb_save_checkpoint(self._h, os.fsencode(path)))
+
+    def load_checkpoint(self, path) -> None:
+        self._check(self._lib.iblb_load_checkpoint(self._h, os.fsencode(path)))
+        self.ns = int(np.fromfile(path, dtype=np.int64, count=9, offset=8)[7])
+
     # -- RCCL group ---------------------------------------------------------------------------
     def attach_rccl(self, unique_id: bytes, nranks: int, rank: int) -> None:
         if len(unique_id) != L.UNIQUE_ID_BYTES:
             raise ValueError("unique id must be 128 bytes")
         self._check(self._lib.iblb_attach_rccl(self._h, unique_id, int(nranks), int(rank)))
+        self.rank = int(rank)
+
+    def gather_macro(self, root: int = 0):
+        """Whole-lattice rho [nx*ny], u [2*nx*ny] on rank `root` (None elsewhere); collective."""
+        n = self.nx * self.ny
+        rho, u = np.empty(n), np.empty(2 * n)
+        self._check(self._lib.iblb_gather_macro(self._h, int(root), _ptr(rho), _ptr(u)))
+        return (rho, u) if getattr(self, "rank", 0) == int(root) else (None, None)
 
 
 def rccl_unique_id(lib=None) -> bytes:

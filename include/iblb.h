@@ -217,6 +217,23 @@ int iblb_group_step(iblb_ctx** ctxs, int n, int nsteps);
 int iblb_rccl_unique_id(char id[IBLB_UNIQUE_ID_BYTES]);
 int iblb_attach_rccl(iblb_ctx* ctx, const char id[IBLB_UNIQUE_ID_BYTES], int nranks, int rank);
 
+/* Whole-lattice rho [nx*ny] and u [2*nx*ny] (reference layout, j = y*XDIM + x) on rank `root`
+ * of an RCCL group: the output gather the reference's single-GPU BigData writer needs
+ * (main.cu:938-971) when the lattice is split over GPUs.  Collective; the other ranks may
+ * pass NULL.  A single slab returns iblb_get_macro. */
+int iblb_gather_macro(iblb_ctx* ctx, int root, double* rho, double* u);
+
+/* ---- checkpoint / restart (absent in the reference; its jobs run 1e5+ steps, cilia6.sh) --
+ * iblb_save_checkpoint writes this context's slab: the stored populations in their storage
+ * precision, step count, cumulative flux Q, Lagrangian points and cilia kinematics state
+ * (written to path.tmp, then renamed).  iblb_load_checkpoint restores it into a context
+ * created with the same lattice, slab, precision, tau/tau2 and body force (and enough
+ * max_points); stepping on from there is bit-identical to the uninterrupted run up to the
+ * summation order of the IB spread.  Each rank of a group saves / loads its own file;
+ * restore before iblb_link_local, before or after iblb_attach_rccl. */
+int iblb_save_checkpoint(iblb_ctx* ctx, const char* path);
+int iblb_load_checkpoint(iblb_ctx* ctx, const char* path);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,7 @@ usage: run_group.py NRANKS NX NY STEPS WITH_IB(0/1) PRECISION(f64/f32)
 import json
 import os
 import sys
+import tempfile
 import threading
 
 import numpy as np
@@ -42,32 +43,64 @@ def main():
 
     uid = rccl_unique_id(lib)
     out = [None] * n
+    gathered = [None] * n
+    restarted = [None] * n
     errors = []
+    half = steps // 2
+    tmp = tempfile.mkdtemp(prefix="iblb_ck_")
+    ck = lambda r: os.path.join(tmp, f"ck.rank{r}")
 
+    def guarded(fn):
+        def run(r):
+            try:
+                fn(r)
+            except Exception as e:  # a failed rank would leave the others waiting: report and exit hard
+                errors.append(f"rank {r}: {e!r}")
+                print(json.dumps({"ok": False, "errors": errors}), flush=True)
+                os._exit(2)
+        return run
+
+    @guarded
     def worker(r):
-        try:
-            xb, xc = plan_slabs(nx, n)[r]
-            lat = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, x_begin=xb,
-                          x_count=xc, lib=lib)
-            lat.set_state(split_state(rho, 1, nx, ny, xb, xc), split_state(u, 2, nx, ny, xb, xc))
-            lat.attach_rccl(uid, n, r)
-            for it in range(steps):
-                if with_ib:
-                    lat.set_lagrangian(*pts(it))
-                lat.step(1)
-            rs, us = lat.macro()
-            out[r] = (xb, xc, rs, us, lat.flux)
-            lat.close()
-        except Exception as e:  # a failed rank would leave the others waiting: report and exit hard
-            errors.append(f"rank {r}: {e!r}")
-            print(json.dumps({"ok": False, "errors": errors}), flush=True)
-            os._exit(2)
+        xb, xc = plan_slabs(nx, n)[r]
+        lat = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, x_begin=xb,
+                      x_count=xc, lib=lib)
+        lat.set_state(split_state(rho, 1, nx, ny, xb, xc), split_state(u, 2, nx, ny, xb, xc))
+        lat.attach_rccl(uid, n, r)
+        for it in range(steps):
+            if it == half:
+                lat.save_checkpoint(ck(r))
+            if with_ib:
+                lat.set_lagrangian(*pts(it))
+            lat.step(1)
+        rs, us = lat.macro()
+        out[r] = (xb, xc, rs, us, lat.flux)
+        gathered[r] = lat.gather_macro(0)  # collective output gather to rank 0
+        lat.close()
 
-    th = [threading.Thread(target=worker, args=(r,)) for r in range(n)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
+    uid2 = rccl_unique_id(lib)
+
+    @guarded
+    def resume(r):  # fresh contexts: attach, restore the mid-run checkpoint, finish the run
+        xb, xc = plan_slabs(nx, n)[r]
+        lat = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, x_begin=xb,
+                      x_count=xc, lib=lib)
+        lat.attach_rccl(uid2, n, r)
+        lat.load_checkpoint(ck(r))
+        for it in range(half, steps):
+            if with_ib:
+                lat.set_lagrangian(*pts(it))
+            lat.step(1)
+        rs, us = lat.macro()
+        restarted[r] = (rs, us, lat.flux, lat.steps)
+        lat.close()
+
+    for fn in (worker, resume):
+        th = [threading.Thread(target=fn, args=(r,)) for r in range(n)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
     R = np.empty((ny, nx))
     U = np.empty((2, ny, nx))
     for xb, xc, rs, us, _ in out:
@@ -83,7 +116,21 @@ def main():
     ok = d_rho <= tol and d_u <= tol and d_q <= 1e-12
     if not with_ib:  # same per-cell arithmetic, halos carry identical values: bit-identical
         ok = ok and exact
+    # the gather reproduces the assembled slabs on rank 0 only
+    g_ok = bool(np.array_equal(gathered[0][0], R) and np.array_equal(gathered[0][1], U)
+                and all(g == (None, None) for g in gathered[1:]))
+    # restart: same steps, same fields as the uninterrupted run (bit-identical without IB; the
+    # IB spread's atomic summation order may differ in the last bit)
+    rs_ok = all(restarted[r][3] == steps for r in range(n))
+    d_re = 0.0
+    for r in range(n):
+        a, b = out[r], restarted[r]
+        d_re = max(d_re, float(np.max(np.abs(a[2] - b[0]))), float(np.max(np.abs(a[3] - b[1]))))
+        rs_ok = rs_ok and abs(a[4] - b[2]) <= 1e-12 * max(abs(a[4]), 1e-300)
+    rs_ok = rs_ok and (d_re == 0.0 if not with_ib else d_re <= 1e-12)
+    ok = ok and g_ok and rs_ok
     print(json.dumps({"ok": bool(ok), "exact": exact, "d_rho": d_rho, "d_u": d_u, "d_flux": d_q, "n": n,
+                      "gather_ok": g_ok, "restart_ok": bool(rs_ok), "d_restart": d_re,
                       "with_ib": with_ib, "precision": prec}), flush=True)
     sys.exit(0 if ok else 1)
 

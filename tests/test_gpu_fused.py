@@ -307,3 +307,58 @@ def test_reference_cilia_scenario(gpu, oracle, precision):
     tol = 1e-9 if precision == "f64" else TOL32
     assert max(r["rho"], r["ux"], r["uy"]) <= tol, r
     assert abs(lat.flux - sim.flux) <= (1e-9 if precision == "f64" else 1e-3) * abs(sim.flux)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("ib", ["none", "cilia"])
+def test_checkpoint_restart(gpu, tmp_path, precision, ib):
+    """iblb_save_checkpoint / iblb_load_checkpoint: a fresh context restored mid-run and stepped
+    on gives the uninterrupted run's fields and flux — bit-identical without IB; with the
+    device cilia within the IB spread's atomic-summation round-off."""
+    from cuda_iblb_11_amd import workloads as W
+    nx, ny, steps, half = 288, 192, 16, 7
+    kw = dict(precision=precision, body_force=W.BODY_FORCE, max_points=576 if ib == "cilia" else 0)
+    rho0, u0 = W.perturbed_state(nx, ny, 7)
+
+    def fresh():
+        lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)
+        if ib == "cilia":
+            lat.set_cilia(6, 48.0, 100000, 100000 // 6)
+        return lat
+
+    a = fresh()
+    a.set_state(rho0, u0)
+    a.step(half)
+    ck = str(tmp_path / "state.ck")
+    a.save_checkpoint(ck)
+    a.step(steps - half)
+    r1, v1 = a.macro()
+    q1 = a.flux
+    b = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)  # cilia configuration comes from the file
+    b.load_checkpoint(ck)
+    assert b.steps == half
+    b.step(steps - half)
+    assert b.steps == steps
+    r2, v2 = b.macro()
+    if ib == "none":
+        assert np.array_equal(r1, r2) and np.array_equal(v1, v2) and b.flux == q1
+    else:
+        assert np.max(np.abs(r1 - r2)) <= 1e-13 and np.max(np.abs(v1 - v2)) <= 1e-13
+        assert abs(b.flux - q1) <= 1e-12 * abs(q1)
+        assert all(np.array_equal(x, y) for x, y in zip(a.lagrangian(), b.lagrangian()))
+
+
+def test_checkpoint_refuses_mismatch(gpu, tmp_path):
+    from cuda_iblb_11_amd import workloads as W
+    a = gpu.Lattice(64, 130, W.TAU, W.TAU2)
+    a.set_state()
+    with pytest.raises(gpu.IblbError):
+        a.save_checkpoint(str(tmp_path / "boot.ck"))  # nothing stepped yet
+    a.step(2)
+    a.save_checkpoint(str(tmp_path / "s.ck"))
+    for other in (gpu.Lattice(64, 128, W.TAU, W.TAU2), gpu.Lattice(64, 130, W.TAU, W.TAU2, precision="f32"),
+                  gpu.Lattice(64, 130, W.TAU + 0.1, W.TAU2)):
+        with pytest.raises(gpu.IblbError):
+            other.load_checkpoint(str(tmp_path / "s.ck"))
+    with pytest.raises(gpu.IblbError):
+        a.load_checkpoint(str(tmp_path / "missing.ck"))
