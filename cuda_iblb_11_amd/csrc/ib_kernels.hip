@@ -8,7 +8,7 @@
 // per-(column, chunk) flags tell the collide-stream kernel where the dense force must be
 // read (it clears values and flag).
 //
-// Single slab: one lane per point does nodes -> F_s -> spread (ib_point_kernel).  Slab
+// Single slab: one 16-lane group per point does nodes -> F_s -> spread (ib_point_kernel).  Slab
 // groups split it so a point's nine nodes may live on different slabs: ib_nodes writes
 // (rho, u_x, u_y) of the nodes this slab owns (zeros elsewhere; a sum over slabs yields
 // every node exactly once), ib_interp_spread accumulates F_s in the reference's node
@@ -62,58 +62,89 @@ hipError_t launch_ib_nodes(const T* g, Layout L, Halo<T> H, int nx, int x_begin,
     return hipGetLastError();
 }
 
-// One point, all of it: its nine nodes' rho and u_raw pulled from g (ImmersedBoundary.cu:117-128
-// via macro, LatticeBoltzmann.cu:396-405), F_s in the reference's order and float rounding, then
-// its 3x3 spread into the dense force (ImmersedBoundary.cu:189-198).  Points are independent
-// (a point's spread needs only its own F_s), so a single-slab step needs one IB launch.
-__device__ __forceinline__ void spread_point(const Layout& L, int nx, int x_begin, int x0, int y0, float xs,
-                                             float ys, float Fx, float Fy, int e, double* __restrict__ fd, long fplane,
-                                             uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
+// One point per 16-lane group, one of its nine nodes per lane (lanes 9-15 idle): node n's rho
+// and u_raw pulled from g (ImmersedBoundary.cu:117-128 via macro, LatticeBoltzmann.cu:396-405)
+// and its interpolation term; F_s accumulated in the reference's node order and float rounding
+// (every lane of the group folds the nine terms itself); then node n's share of the spread
+// (ImmersedBoundary.cu:189-198) into the dense force.  Points are independent (a point's spread
+// needs only its own F_s), so a single-slab step needs one IB launch.
+constexpr int LANES_PER_POINT = 16;
+
+// node (x, y) of a point's 3x3 spread, clipped to the lattice (no periodic image, as the
+// reference's cell-centric gather) and to this slab's columns
+__device__ __forceinline__ void spread_node(const Layout& L, int nx, int x_begin, int x, int y, float xs, float ys,
+                                            float Fx, float Fy, int e, double* __restrict__ fd, long fplane,
+                                            uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
 #pragma clang fp contract(off)
-    if (e == 0) return;
-    for (int n = 0; n < 9; ++n) {
-        const int x = x0 + cx(n), y = y0 + cy(n);
-        if (x < 0 || x >= nx || y < 0 || y >= L.ny) continue;
-        const int xc = x - x_begin;
-        if (xc < 0 || xc >= L.ncol) continue;
-        const float del = d_delta(xs, ys, x, y);
-        if (del == 0.f) continue;
-        const long o = (long)xc * L.col + y;
-        atomicAdd(fd + o, (double)(Fx * del) * 1. * (double)e);
-        atomicAdd(fd + fplane + o, (double)(Fy * del) * 1. * (double)e);
-        flags[(long)xc * nch + y / rows_per_chunk] = 1;
+    if (e == 0 || x < 0 || x >= nx || y < 0 || y >= L.ny) return;
+    const int xc = x - x_begin;
+    if (xc < 0 || xc >= L.ncol) return;
+    const float del = d_delta(xs, ys, x, y);
+    if (del == 0.f) return;
+    const long o = (long)xc * L.col + y;
+    atomicAdd(fd + o, (double)(Fx * del) * 1. * (double)e);
+    atomicAdd(fd + fplane + o, (double)(Fy * del) * 1. * (double)e);
+    flags[(long)xc * nch + y / rows_per_chunk] = 1;
+}
+
+// F_s of the group's point from the per-lane node terms, in node order 0..8
+__device__ __forceinline__ void fold_terms(double tx, double ty, bool valid, float& Fx, float& Fy) {
+#pragma clang fp contract(off)
+    Fx = 0.f;
+    Fy = 0.f;
+#pragma unroll
+    for (int m = 0; m < 9; ++m) {
+        const double ax = __shfl(tx, m, LANES_PER_POINT);
+        const double ay = __shfl(ty, m, LANES_PER_POINT);
+        if (__shfl((int)valid, m, LANES_PER_POINT)) {
+            Fx = (float)((double)Fx + ax);
+            Fy = (float)((double)Fy + ay);
+        }
     }
 }
 
 template <typename T>
-__global__ void ib_point_kernel(const T* __restrict__ g, Layout L, Halo<T> H, int nx, int ns,
-                                const float* __restrict__ s, const float* __restrict__ u_s,
-                                const int* __restrict__ eps, float* __restrict__ F_s, double* __restrict__ fd,
-                                long fplane, uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
+__global__ __launch_bounds__(256) void ib_point_kernel(const T* __restrict__ g, Layout L, Halo<T> H, int nx, int ns,
+                                                       const float* __restrict__ s, const float* __restrict__ u_s,
+                                                       const int* __restrict__ eps, float* __restrict__ F_s,
+                                                       double* __restrict__ fd, long fplane,
+                                                       uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
 #pragma clang fp contract(off)
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ns) return;
-    const float xs = s[2 * k + 0], ys = s[2 * k + 1];
-    const int x0 = node_x0(xs), y0 = node_x0(ys);
-    const double usx = u_s[2 * k + 0], usy = u_s[2 * k + 1];
-    float Fx = 0.f, Fy = 0.f;
-    for (int n = 0; n < 9; ++n) {
-        const int x = x0 + cx(n), y = y0 + cy(n);
+    const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = (int)(tid / LANES_PER_POINT), n = (int)(tid % LANES_PER_POINT);
+    const bool pt = k < ns;  // no early exit: the whole group takes part in the shuffles
+    float xs = 0.f, ys = 0.f;
+    int x = 0, y = 0;
+    double tx = 0., ty = 0.;
+    bool valid = false;
+    if (pt && n < 9) {
+        xs = s[2 * k + 0];
+        ys = s[2 * k + 1];
+        x = node_x0(xs) + cx(n);
+        y = node_x0(ys) + cy(n);
         const long j = (long)y * nx + x;
-        if (j < 0 || j >= (long)nx * L.ny) continue;
-        const int xj = (int)(j % nx), yj = (int)(j / nx);
-        double f[9];
+        if (j >= 0 && j < (long)nx * L.ny) {
+            const int xj = (int)(j % nx), yj = (int)(j / nx);
+            double f[9];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) f[q] = Store<T>::to_f(pull<T>(g, L, H, xj, yj, q), q);
-        double r, mx, my;
-        moments<double>(f, r, mx, my);
-        const double del = d_delta(xs, ys, x, y);
-        Fx = (float)((double)Fx + 2. * (1. * 1. * del) * r * (usx - mx / r));
-        Fy = (float)((double)Fy + 2. * (1. * 1. * del) * r * (usy - my / r));
+            for (int q = 0; q < 9; ++q) f[q] = Store<T>::to_f(pull<T>(g, L, H, xj, yj, q), q);
+            double r, mx, my;
+            moments<double>(f, r, mx, my);
+            const double del = d_delta(xs, ys, x, y);
+            const double usx = u_s[2 * k + 0], usy = u_s[2 * k + 1];
+            tx = 2. * (1. * 1. * del) * r * (usx - mx / r);
+            ty = 2. * (1. * 1. * del) * r * (usy - my / r);
+            valid = true;
+        }
     }
-    F_s[2 * k + 0] = Fx;
-    F_s[2 * k + 1] = Fy;
-    spread_point(L, nx, 0, x0, y0, xs, ys, Fx, Fy, eps ? eps[k] : 1, fd, fplane, flags, nch, rows_per_chunk);
+    float Fx, Fy;
+    fold_terms(tx, ty, valid, Fx, Fy);
+    if (!pt || n >= 9) return;
+    if (n == 0) {
+        F_s[2 * k + 0] = Fx;
+        F_s[2 * k + 1] = Fy;
+    }
+    spread_node(L, nx, 0, x, y, xs, ys, Fx, Fy, eps ? eps[k] : 1, fd, fplane, flags, nch, rows_per_chunk);
 }
 
 template <typename T>
@@ -121,46 +152,63 @@ hipError_t launch_ib_point(const T* g, Layout L, Halo<T> H, int nx, int ns, cons
                            const int* eps, float* F_s, double* fdense, long fplane, uint8_t* flags, int nch,
                            int rows_per_chunk, hipStream_t st) {
     if (ns <= 0) return hipSuccess;
-    ib_point_kernel<T><<<(unsigned)((ns + 127) / 128), 128, 0, st>>>(g, L, H, nx, ns, s, u_s, eps, F_s, fdense, fplane,
-                                                                      flags, nch, rows_per_chunk);
+    const long n = (long)LANES_PER_POINT * ns;
+    ib_point_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(g, L, H, nx, ns, s, u_s, eps, F_s, fdense, fplane,
+                                                                     flags, nch, rows_per_chunk);
     return hipGetLastError();
 }
 
 // Slab groups: F_s from the node values summed over slabs, then the point's spread clipped to
-// this slab's columns.
-__global__ void ib_interp_spread_kernel(Layout L, int nx, int x_begin, int ns, const float* __restrict__ s,
-                                        const float* __restrict__ u_s, const int* __restrict__ eps,
-                                        const double* __restrict__ nv, float* __restrict__ F_s,
-                                        double* __restrict__ fd, long fplane, uint8_t* __restrict__ flags, int nch,
-                                        int rows_per_chunk) {
+// this slab's columns (same lane mapping).
+__global__ __launch_bounds__(256) void ib_interp_spread_kernel(Layout L, int nx, int x_begin, int ns,
+                                                               const float* __restrict__ s,
+                                                               const float* __restrict__ u_s,
+                                                               const int* __restrict__ eps,
+                                                               const double* __restrict__ nv, float* __restrict__ F_s,
+                                                               double* __restrict__ fd, long fplane,
+                                                               uint8_t* __restrict__ flags, int nch,
+                                                               int rows_per_chunk) {
 #pragma clang fp contract(off)
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ns) return;
-    const float xs = s[2 * k + 0], ys = s[2 * k + 1];
-    const int x0 = node_x0(xs), y0 = node_x0(ys);
-    float Fx = 0.f, Fy = 0.f;
-    const double usx = u_s[2 * k + 0], usy = u_s[2 * k + 1];
-    for (int n = 0; n < 9; ++n) {
-        const int x = x0 + cx(n), y = y0 + cy(n);
+    const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = (int)(tid / LANES_PER_POINT), n = (int)(tid % LANES_PER_POINT);
+    const bool pt = k < ns;
+    float xs = 0.f, ys = 0.f;
+    int x = 0, y = 0;
+    double tx = 0., ty = 0.;
+    bool valid = false;
+    if (pt && n < 9) {
+        xs = s[2 * k + 0];
+        ys = s[2 * k + 1];
+        x = node_x0(xs) + cx(n);
+        y = node_x0(ys) + cy(n);
         const long j = (long)y * nx + x;
-        if (j < 0 || j >= (long)nx * L.ny) continue;
-        const double del = d_delta(xs, ys, x, y);
-        const double* v = nv + 27L * k + 3 * n;
-        Fx = (float)((double)Fx + 2. * (1. * 1. * del) * v[0] * (usx - v[1]));
-        Fy = (float)((double)Fy + 2. * (1. * 1. * del) * v[0] * (usy - v[2]));
+        if (j >= 0 && j < (long)nx * L.ny) {
+            const double del = d_delta(xs, ys, x, y);
+            const double* v = nv + 27L * k + 3 * n;
+            const double usx = u_s[2 * k + 0], usy = u_s[2 * k + 1];
+            tx = 2. * (1. * 1. * del) * v[0] * (usx - v[1]);
+            ty = 2. * (1. * 1. * del) * v[0] * (usy - v[2]);
+            valid = true;
+        }
     }
-    F_s[2 * k + 0] = Fx;
-    F_s[2 * k + 1] = Fy;
-    spread_point(L, nx, x_begin, x0, y0, xs, ys, Fx, Fy, eps ? eps[k] : 1, fd, fplane, flags, nch, rows_per_chunk);
+    float Fx, Fy;
+    fold_terms(tx, ty, valid, Fx, Fy);
+    if (!pt || n >= 9) return;
+    if (n == 0) {
+        F_s[2 * k + 0] = Fx;
+        F_s[2 * k + 1] = Fy;
+    }
+    spread_node(L, nx, x_begin, x, y, xs, ys, Fx, Fy, eps ? eps[k] : 1, fd, fplane, flags, nch, rows_per_chunk);
 }
 
 hipError_t launch_ib_interp_spread(Layout L, int nx, int x_begin, int ns, const float* s, const float* u_s,
                                    const int* eps, const double* node_vals, float* F_s, double* fdense, long fplane,
                                    uint8_t* flags, int nch, int rows_per_chunk, hipStream_t st) {
     if (ns <= 0) return hipSuccess;
-    ib_interp_spread_kernel<<<(unsigned)((ns + 127) / 128), 128, 0, st>>>(L, nx, x_begin, ns, s, u_s, eps, node_vals,
-                                                                          F_s, fdense, fplane, flags, nch,
-                                                                          rows_per_chunk);
+    const long n = (long)LANES_PER_POINT * ns;
+    ib_interp_spread_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(L, nx, x_begin, ns, s, u_s, eps, node_vals,
+                                                                         F_s, fdense, fplane, flags, nch,
+                                                                         rows_per_chunk);
     return hipGetLastError();
 }
 
