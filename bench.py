@@ -67,6 +67,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU sample duration")
     p.add_argument("--no-profile-events", action="store_true", help="skip per-launch HIP events")
+    p.add_argument("--rccl-self", action="store_true",
+                   help="N=1 rehearsal of the multi-GPU schedule: the slab is its own RCCL neighbour")
     p.add_argument("--same-device", action="store_true",
                    help="testing only: every rank uses device 0 (exercise the RCCL slab path on one GPU)")
     return p.parse_args()
@@ -166,6 +168,9 @@ def main():
         uid = [P.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         lat.attach_rccl(uid[0], world, rank)
+    elif a.rccl_self:
+        os.environ["IBLB_RCCL_SELF"] = "1"
+        lat.attach_rccl(P.rccl_unique_id(), 1, 0)
     if points is not None:
         lat.set_lagrangian(*points)
 
@@ -237,7 +242,8 @@ def main():
                             f"TRT+Guo, reference TAU/TAU2; one fused pull-stream+collide launch per step"
                             + (f"; IB: {ns} static Lagrangian points, interpolate+spread every step" if ns else ""),
                 "nx": nx, "ny": ny, "global_cells": cells, "ib_points": ns,
-                "parallelism": f"x-slab x{world}" + (" (RCCL halo)" if world > 1 else ""),
+                "parallelism": f"x-slab x{world}" + (" (RCCL halo)" if world > 1 else "")
+                               + (" (RCCL self-ring rehearsal)" if a.rccl_self and world == 1 else ""),
             },
             "ib_ms_per_step": round(tm["ib_ms"] / a.steps, 5) if ns else None,
             "achieved_hbm_gbps": round(mlups * 1e6 * bytes_per_cell / 1e9, 1),

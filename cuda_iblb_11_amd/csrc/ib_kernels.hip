@@ -9,10 +9,8 @@
 // read (it clears values and flag).
 //
 // Single slab: one 16-lane group per point does nodes -> F_s -> spread (ib_point_kernel).  Slab
-// groups split it so a point's nine nodes may live on different slabs: ib_nodes writes
-// (rho, u_x, u_y) of the nodes this slab owns (zeros elsewhere; a sum over slabs yields
-// every node exactly once), ib_interp_spread accumulates F_s in the reference's node
-// order and float rounding and spreads into the owned columns.
+// groups: each slab evaluates every point that spreads into it from a 2-column-deep IB halo
+// (ib_slab_kernel, iblb_device.h IbHalo) — no collective per step.
 #include "iblb_kernels.h"
 
 namespace iblb {
@@ -20,47 +18,6 @@ namespace iblb {
 namespace {
 __device__ __forceinline__ int node_x0(float xs) { return (int)nearbyint((double)xs); }
 }  // namespace
-
-// One lane per (point k, node n).  Flat index j = y*XDIM + x without periodic wrap
-// (ImmersedBoundary.cu:119-122): x = -1 addresses the previous row's last cell, like
-// the reference; j outside [0, XDIM*YDIM) is undefined there and skipped here.
-template <typename T>
-__global__ void ib_nodes_kernel(const T* __restrict__ g, Layout L, Halo<T> H, int nx, int x_begin, int ns,
-                                const float* __restrict__ s, double* __restrict__ nv) {
-#pragma clang fp contract(off)
-    const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (id >= 9L * ns) return;
-    const int k = (int)(id / 9), n = (int)(id - 9L * (id / 9));
-    const float xs = s[2 * k + 0], ys = s[2 * k + 1];
-    const int x = node_x0(xs) + cx(n), y = node_x0(ys) + cy(n);
-    const long j = (long)y * nx + x;
-    double r = 0., ux = 0., uy = 0.;
-    if (j >= 0 && j < (long)nx * L.ny) {
-        const int xj = (int)(j % nx), yj = (int)(j / nx);
-        const int xc = xj - x_begin;
-        if (xc >= 0 && xc < L.ncol) {
-            double f[9];
-#pragma unroll
-            for (int q = 0; q < 9; ++q) f[q] = Store<T>::to_f(pull<T>(g, L, H, xc, yj, q), q);
-            double mx, my;
-            moments<double>(f, r, mx, my);
-            ux = mx / r;  // LatticeBoltzmann.cu:404-405
-            uy = my / r;
-        }
-    }
-    nv[3 * id + 0] = r;
-    nv[3 * id + 1] = ux;
-    nv[3 * id + 2] = uy;
-}
-
-template <typename T>
-hipError_t launch_ib_nodes(const T* g, Layout L, Halo<T> H, int nx, int x_begin, int ns, const float* s,
-                           double* node_vals, hipStream_t st) {
-    if (ns <= 0) return hipSuccess;
-    const long n = 9L * ns;
-    ib_nodes_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(g, L, H, nx, x_begin, ns, s, node_vals);
-    return hipGetLastError();
-}
 
 // One point per 16-lane group, one of its nine nodes per lane (lanes 9-15 idle): node n's rho
 // and u_raw pulled from g (ImmersedBoundary.cu:117-128 via macro, LatticeBoltzmann.cu:396-405)
@@ -158,79 +115,114 @@ hipError_t launch_ib_point(const T* g, Layout L, Halo<T> H, int nx, int ns, cons
     return hipGetLastError();
 }
 
-// Slab groups: F_s from the node values summed over slabs, then the point's spread clipped to
-// this slab's columns (same lane mapping).
-__global__ __launch_bounds__(256) void ib_interp_spread_kernel(Layout L, int nx, int x_begin, int ns,
-                                                               const float* __restrict__ s,
-                                                               const float* __restrict__ u_s,
-                                                               const int* __restrict__ eps,
-                                                               const double* __restrict__ nv, float* __restrict__ F_s,
-                                                               double* __restrict__ fd, long fplane,
-                                                               uint8_t* __restrict__ flags, int nch,
-                                                               int rows_per_chunk) {
+// Slab groups: every slab evaluates, by itself, each point that spreads into it — the point's
+// nine nodes lie within 2 columns of the slab and are pulled through the IB halo (IbHalo) —
+// and spreads into its own columns.  A point straddling two slabs is evaluated by both with
+// the same data in the same order, so the force is bit-identical to a single slab; F_s is
+// reported by the slab holding column min(x0, XDIM-1) (zeros elsewhere: the reader sums).
+// Needs the reference's invariant 0 <= nearbyint(xs) <= XDIM (boundary_check, main.cu:202-205).
+template <typename T>
+__global__ __launch_bounds__(256) void ib_slab_kernel(const T* __restrict__ g, Layout L, IbHalo<T> X, int nx,
+                                                      int x_begin, int ns, const float* __restrict__ s,
+                                                      const float* __restrict__ u_s, const int* __restrict__ eps,
+                                                      float* __restrict__ F_s, double* __restrict__ fd, long fplane,
+                                                      uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
 #pragma clang fp contract(off)
     const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const int k = (int)(tid / LANES_PER_POINT), n = (int)(tid % LANES_PER_POINT);
     const bool pt = k < ns;
     float xs = 0.f, ys = 0.f;
-    int x = 0, y = 0;
-    double tx = 0., ty = 0.;
-    bool valid = false;
-    if (pt && n < 9) {
+    int x0 = 0, x = 0, y = 0;
+    bool mine = false;
+    if (pt) {
         xs = s[2 * k + 0];
         ys = s[2 * k + 1];
-        x = node_x0(xs) + cx(n);
+        x0 = node_x0(xs);
+        for (int dx = -1; dx <= 1; ++dx) {  // group-uniform: does the point spread into this slab?
+            const int xx = x0 + dx;
+            mine |= xx >= 0 && xx < nx && xx >= x_begin && xx < x_begin + L.ncol;
+        }
+    }
+    double tx = 0., ty = 0.;
+    bool valid = false;
+    if (mine && n < 9) {
+        x = x0 + cx(n);
         y = node_x0(ys) + cy(n);
         const long j = (long)y * nx + x;
         if (j >= 0 && j < (long)nx * L.ny) {
-            const double del = d_delta(xs, ys, x, y);
-            const double* v = nv + 27L * k + 3 * n;
-            const double usx = u_s[2 * k + 0], usy = u_s[2 * k + 1];
-            tx = 2. * (1. * 1. * del) * v[0] * (usx - v[1]);
-            ty = 2. * (1. * 1. * del) * v[0] * (usy - v[2]);
-            valid = true;
+            const int xj = (int)(j % nx), yj = (int)(j / nx);
+            int xl = xj - x_begin;  // slab-local node column, periodic
+            if (xl < -2) xl += nx;
+            else if (xl > L.ncol + 1) xl -= nx;
+            if (xl >= -2 && xl <= L.ncol + 1) {
+                double f[9];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) f[q] = Store<T>::to_f(pull_ib<T>(g, L, X, xl, yj, q), q);
+                double r, mx, my;
+                moments<double>(f, r, mx, my);
+                const double del = d_delta(xs, ys, x, y);
+                const double usx = u_s[2 * k + 0], usy = u_s[2 * k + 1];
+                tx = 2. * (1. * 1. * del) * r * (usx - mx / r);
+                ty = 2. * (1. * 1. * del) * r * (usy - my / r);
+                valid = true;
+            }
         }
     }
     float Fx, Fy;
     fold_terms(tx, ty, valid, Fx, Fy);
     if (!pt || n >= 9) return;
     if (n == 0) {
-        F_s[2 * k + 0] = Fx;
-        F_s[2 * k + 1] = Fy;
+        const int xo = x0 < nx - 1 ? x0 : nx - 1;
+        const bool owner = xo >= x_begin && xo < x_begin + L.ncol;
+        F_s[2 * k + 0] = owner ? Fx : 0.f;
+        F_s[2 * k + 1] = owner ? Fy : 0.f;
     }
-    spread_node(L, nx, x_begin, x, y, xs, ys, Fx, Fy, eps ? eps[k] : 1, fd, fplane, flags, nch, rows_per_chunk);
+    if (mine) spread_node(L, nx, x_begin, x, y, xs, ys, Fx, Fy, eps ? eps[k] : 1, fd, fplane, flags, nch, rows_per_chunk);
 }
 
-hipError_t launch_ib_interp_spread(Layout L, int nx, int x_begin, int ns, const float* s, const float* u_s,
-                                   const int* eps, const double* node_vals, float* F_s, double* fdense, long fplane,
-                                   uint8_t* flags, int nch, int rows_per_chunk, hipStream_t st) {
+template <typename T>
+hipError_t launch_ib_slab(const T* g, Layout L, IbHalo<T> X, int nx, int x_begin, int ns, const float* s,
+                          const float* u_s, const int* eps, float* F_s, double* fdense, long fplane, uint8_t* flags,
+                          int nch, int rows_per_chunk, hipStream_t st) {
     if (ns <= 0) return hipSuccess;
     const long n = (long)LANES_PER_POINT * ns;
-    ib_interp_spread_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(L, nx, x_begin, ns, s, u_s, eps, node_vals,
-                                                                         F_s, fdense, fplane, flags, nch,
-                                                                         rows_per_chunk);
+    ib_slab_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(g, L, X, nx, x_begin, ns, s, u_s, eps, F_s, fdense,
+                                                                    fplane, flags, nch, rows_per_chunk);
     return hipGetLastError();
 }
 
+// Slots 3..IB_HALO_SLOTS-1 of both send buffers from the state g (slots 0-2 are written by
+// the collide that produced g).  One lane per row, one block row per (side, slot).
+template <typename T>
+__global__ void pack_ib_halo_kernel(const T* __restrict__ g, Layout L, T* __restrict__ send_left,
+                                    T* __restrict__ send_right) {
+    const int y = blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = 3 + (int)blockIdx.y, right = (int)blockIdx.z;
+    if (y >= L.ny) return;
+    const int d = send_slot_depth(s), k = send_slot_plane(right != 0, s);
+    const int xc = right ? L.ncol - 1 - d : d;
+    T* dst = right ? send_right : send_left;
+    dst[(long)s * L.col + y] = g[k * L.plane + (long)xc * L.col + y];
+}
+
+template <typename T>
+hipError_t launch_pack_ib_halo(const T* g, Layout L, T* send_left, T* send_right, hipStream_t st) {
+    dim3 grid((unsigned)((L.ny + 255) / 256), IB_HALO_SLOTS - 3, 2);
+    pack_ib_halo_kernel<T><<<grid, 256, 0, st>>>(g, L, send_left, send_right);
+    return hipGetLastError();
+}
+
+template hipError_t launch_ib_slab<double>(const double*, Layout, IbHalo<double>, int, int, int, const float*,
+                                           const float*, const int*, float*, double*, long, uint8_t*, int, int,
+                                           hipStream_t);
+template hipError_t launch_ib_slab<float>(const float*, Layout, IbHalo<float>, int, int, int, const float*,
+                                          const float*, const int*, float*, double*, long, uint8_t*, int, int,
+                                          hipStream_t);
+template hipError_t launch_pack_ib_halo<double>(const double*, Layout, double*, double*, hipStream_t);
+template hipError_t launch_pack_ib_halo<float>(const float*, Layout, float*, float*, hipStream_t);
 template hipError_t launch_ib_point<double>(const double*, Layout, Halo<double>, int, int, const float*, const float*,
                                             const int*, float*, double*, long, uint8_t*, int, int, hipStream_t);
 template hipError_t launch_ib_point<float>(const float*, Layout, Halo<float>, int, int, const float*, const float*,
                                            const int*, float*, double*, long, uint8_t*, int, int, hipStream_t);
-
-__global__ void sum_into_kernel(double* __restrict__ dst, const double* __restrict__ src, long n) {
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dst[i] += src[i];
-}
-
-hipError_t launch_sum_into(double* dst, const double* src, long n, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    sum_into_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(dst, src, n);
-    return hipGetLastError();
-}
-
-template hipError_t launch_ib_nodes<double>(const double*, Layout, Halo<double>, int, int, int, const float*, double*,
-                                            hipStream_t);
-template hipError_t launch_ib_nodes<float>(const float*, Layout, Halo<float>, int, int, int, const float*, double*,
-                                           hipStream_t);
 
 }  // namespace iblb

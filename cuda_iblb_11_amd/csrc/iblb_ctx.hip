@@ -88,8 +88,7 @@ struct iblb_ctx {
     float* d_us = nullptr;
     float* d_Fs = nullptr;
     int* d_eps = nullptr;
-    double* d_nv = nullptr;
-    double* d_nv_tmp = nullptr;
+    float* d_Fs_sum = nullptr;  // F_s summed over an RCCL group (reader scratch)
     double* fdense = nullptr;
     uint8_t* flags = nullptr;
     // flux: d_Q[0] cumulative, d_Q[1] scratch
@@ -99,12 +98,15 @@ struct iblb_ctx {
     long long t = 0;
     int ib_state = IB_NONE;
     bool halo_valid = false;
+    bool halo_ib = false;  // the received halo carries the IB slots (IB_HALO_SLOTS)
+    int halo_slots = HALO_SLOTS;  // slots per halo buffer (IB_HALO_SLOTS when IB-capable)
     // transport
     int transport = TR_NONE;
     iblb_ctx* left = nullptr;
     iblb_ctx* right = nullptr;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    bool self_ring = false;  // one rank that is its own neighbour over RCCL (IBLB_RCCL_SELF, rehearsal)
     std::vector<int> slab_begin, slab_count;  // every rank's columns (RCCL group)
     hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with the interior
     hipEvent_t ev_bnd = nullptr;        // boundary columns + send buffers of the state written
@@ -149,8 +151,10 @@ int hip_fail(iblb_ctx* c, hipError_t e, const char* what) {
 template <typename T>
 T* gptr(iblb_ctx* c, int which) { return (T*)c->g[which]; }
 
-bool single_slab(const iblb_ctx* c) { return c->ncol == c->nx && c->transport != TR_LOCAL && c->nranks <= 1; }
-bool rccl_multi(const iblb_ctx* c) { return c->transport == TR_RCCL && c->nranks > 1; }
+bool single_slab(const iblb_ctx* c) {
+    return c->ncol == c->nx && c->transport != TR_LOCAL && c->nranks <= 1 && !c->self_ring;
+}
+bool rccl_multi(const iblb_ctx* c) { return c->transport == TR_RCCL && (c->nranks > 1 || c->self_ring); }
 bool ib_active(const iblb_ctx* c) { return c->max_points > 0 && c->ns > 0; }
 
 template <typename T>
@@ -223,11 +227,23 @@ int ev_end(iblb_ctx* c, size_t idx, int kind, long long cells = 0, hipStream_t s
 }
 
 // ---- halo exchange ----------------------------------------------------------------------
-int exchange_rccl(iblb_ctx* c, hipStream_t st) {
+// IB slots of the send buffers (slots 0-2 come from the collide)
+template <typename T>
+int pack_ib(iblb_ctx* c, hipStream_t st) {
+    HIP_TRY(c, launch_pack_ib_halo<T>(gptr<T>(c, c->cur), c->L, (T*)c->send_left, (T*)c->send_right, st));
+    return IBLB_OK;
+}
+int pack_ib_any(iblb_ctx* c, hipStream_t st) {
+    return c->prec == IBLB_PREC_F64 ? pack_ib<double>(c, st) : pack_ib<float>(c, st);
+}
+
+// ib: also carry the IB slots (the owed force is evaluated from this halo)
+int exchange_rccl(iblb_ctx* c, hipStream_t st, bool ib = false) {
     size_t ev = 0;
-    int rc = ev_begin(c, &ev, st);
-    if (rc) return rc;
-    const size_t n = 3 * (size_t)c->L.col;
+    int rc;
+    if (ib && (rc = pack_ib_any(c, st))) return rc;
+    if ((rc = ev_begin(c, &ev, st))) return rc;
+    const size_t n = (size_t)(ib ? IB_HALO_SLOTS : HALO_SLOTS) * c->L.col;
     const ncclDataType_t dt = c->prec == IBLB_PREC_F64 ? ncclFloat64 : ncclFloat32;
     const int lr = (c->rank + c->nranks - 1) % c->nranks, rr = (c->rank + 1) % c->nranks;
     NCCL_TRY(c, ncclGroupStart());
@@ -237,15 +253,18 @@ int exchange_rccl(iblb_ctx* c, hipStream_t st) {
     NCCL_TRY(c, ncclRecv(c->recv_right, n, dt, rr, c->comm, st));
     NCCL_TRY(c, ncclGroupEnd());
     c->halo_valid = true;
+    c->halo_ib = ib;
     return ev_end(c, ev, EV_HALO, 0, st);
 }
 
-int exchange_local(iblb_ctx* c) {
-    const size_t bytes = 3 * (size_t)c->L.col * c->esize;
+// local group: the neighbours' send buffers are complete (group_exchange packed them)
+int exchange_local(iblb_ctx* c, bool ib) {
+    const size_t bytes = (size_t)(ib ? IB_HALO_SLOTS : HALO_SLOTS) * c->L.col * c->esize;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipMemcpyAsync(c->recv_left, c->left->send_right, bytes, hipMemcpyDefault, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->recv_right, c->right->send_left, bytes, hipMemcpyDefault, c->stream));
     c->halo_valid = true;
+    c->halo_ib = ib;
     return IBLB_OK;
 }
 
@@ -267,25 +286,8 @@ int pack_send(iblb_ctx* c) {
 }
 
 // ---- immersed boundary ------------------------------------------------------------------
-template <typename T>
-int ib_nodes(iblb_ctx* c) {
-    HIP_TRY(c, launch_ib_nodes<T>(gptr<T>(c, c->cur), c->L, halo_of<T>(c, c->cur), c->nx, c->x_begin, c->ns, c->d_s,
-                                  c->d_nv, c->stream));
-    return IBLB_OK;
-}
-
-int ib_nodes_any(iblb_ctx* c) { return c->prec == IBLB_PREC_F64 ? ib_nodes<double>(c) : ib_nodes<float>(c); }
-
-// Slab groups: F_s from the summed node values, spread into this slab.  The dense force and
-// its flags are clean here: the collide that consumed the previous force cleared both.
-int ib_finish(iblb_ctx* c) {
-    HIP_TRY(c, launch_ib_interp_spread(c->L, c->nx, c->x_begin, c->ns, c->d_s, c->d_us, c->d_eps, c->d_nv, c->d_Fs,
-                                       c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream));
-    c->ib_state = IB_READY;
-    return IBLB_OK;
-}
-
-// Single slab: the whole IB of a step in one launch.
+// Single slab: the whole IB of a step in one launch.  The dense force and its flags are clean
+// here: the collide that consumed the previous force cleared both.
 template <typename T>
 int ib_single(iblb_ctx* c) {
     HIP_TRY(c, launch_ib_point<T>(gptr<T>(c, c->cur), c->L, halo_of<T>(c, c->cur), c->nx, c->ns, c->d_s, c->d_us,
@@ -294,10 +296,28 @@ int ib_single(iblb_ctx* c) {
     return IBLB_OK;
 }
 
-// force^t for a context that is alone or in an RCCL group (local groups: group code)
+// Slab of a group: the points spreading into it, from the IB halo (no collective).
+template <typename T>
+int ib_slab(iblb_ctx* c) {
+    IbHalo<T> X{(const T*)c->recv_left, (const T*)c->recv_right};
+    HIP_TRY(c, launch_ib_slab<T>(gptr<T>(c, c->cur), c->L, X, c->nx, c->x_begin, c->ns, c->d_s, c->d_us, c->d_eps,
+                                 c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream));
+    c->ib_state = IB_READY;
+    return IBLB_OK;
+}
+
+int ib_slab_any(iblb_ctx* c) {
+    if (c->ncol < 3) return fail(c, IBLB_ERR_ARG, "immersed boundary across slabs needs >= 3 columns per slab");
+    return c->prec == IBLB_PREC_F64 ? ib_slab<double>(c) : ib_slab<float>(c);
+}
+
+// halo of the current state for a context that is alone or in an RCCL group (local groups:
+// group code); with an owed IB force it must carry the IB slots
 int ensure_halo(iblb_ctx* c) {
-    if (c->halo_valid || single_slab(c)) return IBLB_OK;
-    if (c->transport == TR_RCCL) return exchange_rccl(c, c->stream);
+    if (single_slab(c)) return IBLB_OK;
+    const bool ib = c->ib_state == IB_PENDING;
+    if (c->halo_valid && (c->halo_ib || !ib)) return IBLB_OK;
+    if (c->transport == TR_RCCL) return exchange_rccl(c, c->stream, ib);
     return fail(c, IBLB_ERR_STATE, "slab halo not available: link the slabs (iblb_link_local / iblb_attach_rccl)");
 }
 
@@ -312,9 +332,7 @@ int ensure_force(iblb_ctx* c) {
     if (single_slab(c)) {
         if ((rc = c->prec == IBLB_PREC_F64 ? ib_single<double>(c) : ib_single<float>(c))) return rc;
     } else {
-        if ((rc = ib_nodes_any(c))) return rc;
-        NCCL_TRY(c, ncclAllReduce(c->d_nv, c->d_nv, 27 * (size_t)c->ns, ncclFloat64, ncclSum, c->comm, c->stream));
-        if ((rc = ib_finish(c))) return rc;
+        if ((rc = ib_slab_any(c))) return rc;
     }
     return ev_end(c, ev, EV_IB);
 }
@@ -608,7 +626,8 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     }
     // halo buffers: recv_left, recv_right, send_left, send_right; each 3 slots + guards
     {
-        const size_t slot = (size_t)(3 * col + 2 * GUARD) * c->esize;
+        c->halo_slots = c->max_points > 0 ? IB_HALO_SLOTS : HALO_SLOTS;
+        const size_t slot = (size_t)(c->halo_slots * col + 2 * GUARD) * c->esize;
         int rc = alloc_zero(c, (void**)&c->halo_alloc, 4 * slot);
         if (rc) return bail(rc);
         c->recv_left = c->halo_alloc + 0 * slot + GUARD * c->esize;
@@ -624,8 +643,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
         if ((rc = alloc_zero(c, (void**)&c->d_us, 2 * np * sizeof(float)))) return bail(rc);
         if ((rc = alloc_zero(c, (void**)&c->d_Fs, 2 * np * sizeof(float)))) return bail(rc);
         if ((rc = alloc_zero(c, (void**)&c->d_eps, np * sizeof(int)))) return bail(rc);
-        if ((rc = alloc_zero(c, (void**)&c->d_nv, 27 * np * sizeof(double)))) return bail(rc);
-        if ((rc = alloc_zero(c, (void**)&c->d_nv_tmp, 27 * np * sizeof(double)))) return bail(rc);
+        if ((rc = alloc_zero(c, (void**)&c->d_Fs_sum, 2 * np * sizeof(float)))) return bail(rc);
         if ((rc = alloc_zero(c, (void**)&c->fdense, 2 * (size_t)c->fplane * sizeof(double)))) return bail(rc);
         if ((rc = alloc_zero(c, (void**)&c->flags, (size_t)c->ncol * c->nch))) return bail(rc);
     }
@@ -646,7 +664,7 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->g_alloc) (void)hipFree(c->g_alloc);
     void* bufs[] = {c->cil_samples, c->cil_lasts, c->cil_bpoints,
                     c->halo_alloc, c->rho0, c->u0, c->force0, c->d_s, c->d_us, c->d_Fs,
-                    c->d_eps, c->d_nv, c->d_nv_tmp, c->fdense, c->flags, c->d_Q};
+                    c->d_eps, c->d_Fs_sum, c->fdense, c->flags, c->d_Q};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -725,6 +743,14 @@ int iblb_set_lagrangian(iblb_ctx* c, int ns, const float* s, const float* u_s, c
     if (ns > c->max_points) return fail(c, IBLB_ERR_ARG, "ns exceeds max_points of the context");
     if (ns > 0 && (!s || !u_s)) return IBLB_ERR_ARG;
     if (c->cilia_on) return fail(c, IBLB_ERR_STATE, "cilia kinematics active: points come from iblb_set_cilia");
+    if (ns > 0 && c->ncol != c->nx) {  // a slab of a group evaluates the points spreading into it
+        if (c->ncol < 3) return fail(c, IBLB_ERR_ARG, "immersed boundary across slabs needs >= 3 columns per slab");
+        for (int k = 0; k < ns; ++k) {
+            const double x0 = std::nearbyint((double)s[2 * k]);
+            if (!(x0 >= 0. && x0 <= (double)c->nx))
+                return fail(c, IBLB_ERR_ARG, "slab groups need 0 <= nearbyint(s_x) <= XDIM (main.cu:202-205)");
+        }
+    }
     HIP_TRY(c, hipSetDevice(c->device));
     // force^t still owed to the old points: evaluate it before they change
     if (c->ib_state == IB_PENDING) {
@@ -870,8 +896,13 @@ int iblb_get_lagrangian_force(iblb_ctx* c, float* F_s) {
     if (rc) return rc;
     if (c->ns == 0) return IBLB_OK;
     HIP_TRY(c, hipSetDevice(c->device));
+    const float* src = c->d_Fs;
+    if (rccl_multi(c)) {  // each point's F_s is held by one slab, zeros elsewhere: sum exactly
+        NCCL_TRY(c, ncclAllReduce(c->d_Fs, c->d_Fs_sum, 2 * (size_t)c->ns, ncclFloat32, ncclSum, c->comm, c->stream));
+        src = c->d_Fs_sum;
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    HIP_TRY(c, hipMemcpy(F_s, c->d_Fs, 2 * (size_t)c->ns * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(F_s, src, 2 * (size_t)c->ns * sizeof(float), hipMemcpyDeviceToHost));
     return IBLB_OK;
 }
 
@@ -892,7 +923,7 @@ int iblb_get_flux(iblb_ctx* c, double* Q) {
             HIP_TRY(c, launch_flux<float>(gptr<float>(c, c->cur), c->L, halo_of<float>(c, c->cur), fd, c->fplane,
                                           c->coef.gx, c->coef.gy, fc, c->cfg.flux_norm, c->d_Q + 1, c->stream));
     }
-    if (c->transport == TR_RCCL && c->nranks > 1)
+    if (rccl_multi(c))
         NCCL_TRY(c, ncclAllReduce(c->d_Q + 1, c->d_Q + 1, 1, ncclFloat64, ncclSum, c->comm, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipMemcpy(Q, c->d_Q + 1, sizeof(double), hipMemcpyDeviceToHost));
@@ -989,39 +1020,27 @@ int iblb_link_local(iblb_ctx** ctxs, int n) {
 }
 
 static int group_exchange(iblb_ctx** cs, int n) {
-    int rc = sync_all(cs, n);
-    if (rc) return rc;
+    bool ib = false;  // an owed IB force is evaluated from this halo: carry the IB slots
+    for (int i = 0; i < n; ++i) ib |= cs[i]->ib_state == IB_PENDING;
+    int rc;
+    for (int i = 0; i < n; ++i) {
+        if (ib) {
+            HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
+            if ((rc = pack_ib_any(cs[i], cs[i]->stream))) return rc;
+        }
+    }
+    if ((rc = sync_all(cs, n))) return rc;
     for (int i = 0; i < n; ++i)
-        if ((rc = exchange_local(cs[i]))) return rc;
+        if ((rc = exchange_local(cs[i], ib))) return rc;
     return sync_all(cs, n);
 }
 
 static int group_force(iblb_ctx** cs, int n) {
-    bool pending = false;
-    for (int i = 0; i < n; ++i) pending |= cs[i]->ib_state == IB_PENDING;
-    if (!pending) return IBLB_OK;
     int rc;
     for (int i = 0; i < n; ++i) {
+        if (cs[i]->ib_state != IB_PENDING) continue;
         HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
-        if ((rc = ib_nodes_any(cs[i]))) return rc;
-    }
-    if ((rc = sync_all(cs, n))) return rc;
-    // sum the per-slab node values (each node is owned by exactly one slab)
-    iblb_ctx* c0 = cs[0];
-    const size_t nb = 27 * (size_t)c0->ns * sizeof(double);
-    HIP_TRY(c0, hipSetDevice(c0->device));
-    for (int i = 1; i < n; ++i) {
-        HIP_TRY(c0, hipMemcpyAsync(c0->d_nv_tmp, cs[i]->d_nv, nb, hipMemcpyDefault, c0->stream));
-        HIP_TRY(c0, launch_sum_into(c0->d_nv, c0->d_nv_tmp, 27L * c0->ns, c0->stream));
-    }
-    HIP_TRY(c0, hipStreamSynchronize(c0->stream));
-    for (int i = 1; i < n; ++i) {
-        HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
-        HIP_TRY(cs[i], hipMemcpyAsync(cs[i]->d_nv, c0->d_nv, nb, hipMemcpyDefault, cs[i]->stream));
-    }
-    for (int i = 0; i < n; ++i) {
-        HIP_TRY(cs[i], hipSetDevice(cs[i]->device));
-        if ((rc = ib_finish(cs[i]))) return rc;
+        if ((rc = ib_slab_any(cs[i]))) return rc;
     }
     return sync_all(cs, n);
 }
@@ -1038,7 +1057,8 @@ int iblb_group_step(iblb_ctx** cs, int n, int nsteps) {
     int rc;
     for (int s = 0; s < nsteps; ++s) {
         if (cs[0]->phase == PH_RUN) {
-            if (!cs[0]->halo_valid && (rc = group_exchange(cs, n))) return rc;
+            const bool ib = cs[0]->ib_state == IB_PENDING;
+            if ((!cs[0]->halo_valid || (ib && !cs[0]->halo_ib)) && (rc = group_exchange(cs, n))) return rc;
             if ((rc = group_force(cs, n))) return rc;
         }
         for (int i = 0; i < n; ++i) {
@@ -1079,6 +1099,9 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
     c->nranks = nranks;
     c->rank = rank;
     c->transport = TR_RCCL;
+    // IBLB_RCCL_SELF=1 with one rank: the slab exchanges its halo with itself through RCCL, so
+    // the multi-slab schedule (comm stream, overlap, node all-reduce) runs on one GPU
+    c->self_ring = nranks == 1 && env_long("IBLB_RCCL_SELF", 0) != 0;
     if (nranks > 1) {
         // the slabs must tile the lattice in rank order: check (x_begin, ncol) of all ranks
         DevBuf d;
@@ -1103,6 +1126,12 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
             c->slab_begin[r] = all[2 * r];
             c->slab_count[r] = all[2 * r + 1];
         }
+    } else {
+        if (c->self_ring && c->ncol != c->nx) return fail(c, IBLB_ERR_ARG, "IBLB_RCCL_SELF needs the whole lattice");
+        c->slab_begin.assign(1, c->x_begin);
+        c->slab_count.assign(1, c->ncol);
+    }
+    if (rccl_multi(c)) {
         HIP_TRY(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));

@@ -72,18 +72,18 @@ hipError_t launch_field_out(const double* lay, double* ref, Layout L, int ncomp,
                             double add1, hipStream_t s);
 
 // Immersed boundary (global coordinates; the slab owns columns [x_begin, x_begin+ncol)).
-template <typename T>
-hipError_t launch_ib_nodes(const T* g, Layout L, Halo<T> H, int nx, int x_begin, int ns, const float* s,
-                           double* node_vals, hipStream_t st);
-hipError_t launch_sum_into(double* dst, const double* src, long n, hipStream_t st);
 // Single slab: nodes + interpolation + spread of every point in one launch.
 template <typename T>
 hipError_t launch_ib_point(const T* g, Layout L, Halo<T> H, int nx, int ns, const float* s, const float* u_s,
                            const int* eps, float* F_s, double* fdense, long fplane, uint8_t* flags, int nch,
                            int rows_per_chunk, hipStream_t st);
-// Slab groups: interpolation from summed node values + spread clipped to the slab.
-hipError_t launch_ib_interp_spread(Layout L, int nx, int x_begin, int ns, const float* s, const float* u_s,
-                                   const int* eps, const double* node_vals, float* F_s, double* fdense, long fplane,
-                                   uint8_t* flags, int nch, int rows_per_chunk, hipStream_t st);
+// Slab groups: the points spreading into this slab, nodes pulled through the IB halo.
+template <typename T>
+hipError_t launch_ib_slab(const T* g, Layout L, IbHalo<T> X, int nx, int x_begin, int ns, const float* s,
+                          const float* u_s, const int* eps, float* F_s, double* fdense, long fplane, uint8_t* flags,
+                          int nch, int rows_per_chunk, hipStream_t st);
+// IB halo slots 3.. of both send buffers from the state g.
+template <typename T>
+hipError_t launch_pack_ib_halo(const T* g, Layout L, T* send_left, T* send_right, hipStream_t st);
 
 }  // namespace iblb

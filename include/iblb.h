@@ -154,7 +154,9 @@ int iblb_set_state(iblb_ctx* ctx, const double* rho, const double* u, const doub
                    const double* force);
 
 /* Lagrangian points for the next immersed-boundary evaluation (main.cu:834 boundary_check
- * outputs): s [2ns] xy, u_s [2ns] xy, epsilon [ns] (NULL = all 1).  Global coordinates. */
+ * outputs): s [2ns] xy, u_s [2ns] xy, epsilon [ns] (NULL = all 1).  Global coordinates.
+ * A slab of a group needs >= 3 columns and the reference's invariant 0 <= s_x <= XDIM
+ * (boundary_check wraps s_x into it, main.cu:202-205); IBLB_ERR_ARG otherwise. */
 int iblb_set_lagrangian(iblb_ctx* ctx, int ns, const float* s, const float* u_s,
                         const int* epsilon);
 
@@ -182,7 +184,9 @@ int iblb_get_macro(iblb_ctx* ctx, double* rho, double* u);
 int iblb_get_populations(iblb_ctx* ctx, double* f);
 /* force^t [2N] SoA as the reference's d_force after spread (plus body_force). */
 int iblb_get_force(iblb_ctx* ctx, double* force);
-/* Lagrangian force F_s [2ns] of the last interpolation. */
+/* Lagrangian force F_s [2ns] of the last interpolation.  Collective in an RCCL group; in a
+ * local group each slab holds the F_s of the points whose column min(x0, XDIM-1) it owns and
+ * zeros for the others (sum over the slabs). */
 int iblb_get_lagrangian_force(iblb_ctx* ctx, float* F_s);
 /* Cumulative flux Q (ImmersedBoundary.cu:259-264).  With a multi-slab RCCL group this
  * is the sum over all ranks; with a local group it is this slab's share. */

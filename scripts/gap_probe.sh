@@ -13,6 +13,14 @@ for nx in 4096 1024 512; do
       "$OUT/b_${nx}${ev}.json" $nx "x$ev"
   done
 done
+for nx in 1024 512; do
+  timeout -k 10 200 python bench.py --nx $nx --ny 4096 --steps 400 --warmup 40 --no-cpu-baseline --rccl-self \
+    > "$OUT/s_${nx}.json" 2> "$OUT/s_${nx}.err" || { tail -20 "$OUT/s_${nx}.err"; exit 1; }
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print('self-ring', sys.argv[2], d['ms_per_step'], d['roofline']['launch_ms'])" "$OUT/s_${nx}.json" $nx
+done
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof512s" -o trace \
+  -- python bench.py --nx 512 --ny 4096 --steps 200 --warmup 20 --no-cpu-baseline --no-profile-events --rccl-self > /dev/null 2> "$OUT/prof512s.err" \
+  || { tail -20 "$OUT/prof512s.err"; exit 1; }
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof512" -o trace \
   -- python bench.py --nx 512 --ny 4096 --steps 200 --warmup 20 --no-cpu-baseline --no-profile-events > /dev/null 2> "$OUT/prof512.err" \
   || { tail -20 "$OUT/prof512.err"; exit 1; }

@@ -219,7 +219,7 @@ ncclResult_t ncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int
 
 ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t dt, ncclRedOp_t op,
                            ncclComm_t comm, hipStream_t stream) {
-    if (op != ncclSum || (dt != ncclFloat64 && dt != ncclInt32)) return ncclInvalidUsage;
+    if (op != ncclSum || (dt != ncclFloat64 && dt != ncclFloat32 && dt != ncclInt32)) return ncclInvalidUsage;
     World* w = comm->w;
     const size_t bytes = count * type_size(dt);
     if (hipStreamSynchronize(stream) != hipSuccess) return ncclUnhandledCudaError;
@@ -230,6 +230,7 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
         if (hipMemcpy(tmp.data(), w->slot[r], bytes, hipMemcpyDefault) != hipSuccess) return ncclUnhandledCudaError;
         for (size_t i = 0; i < count; ++i) {
             if (dt == ncclFloat64) ((double*)acc.data())[i] += ((double*)tmp.data())[i];
+            else if (dt == ncclFloat32) ((float*)acc.data())[i] += ((float*)tmp.data())[i];
             else ((int*)acc.data())[i] += ((int*)tmp.data())[i];
         }
     }

@@ -29,7 +29,11 @@ def main():
     rho, u = W.perturbed_state(nx, ny, 31)
     bf = (1e-6, 2e-7)
     edge = plan_slabs(nx, n)[0][1] - 0.4  # filament straddling the slab 0 | slab 1 edge
-    pts = lambda it: W.filament(it, n_points=40, x0=edge, y0=1.0, U0=2e-3, period=30, sway=2.0)
+
+    def pts(it):  # plus one at x = XDIM (nodes wrap to column 0 of the next row)
+        a = W.filament(it, n_points=40, x0=edge, y0=1.0, U0=2e-3, period=30, sway=2.0)
+        b = W.filament(it, n_points=20, x0=nx - 0.3, y0=50.0, U0=2e-3, period=30, sway=0.5)
+        return tuple(np.concatenate([p, q]) for p, q in zip(a, b))
     mp = 64 if with_ib else 0
 
     single = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, lib=lib)
@@ -40,6 +44,7 @@ def main():
         single.step(1)
     r1, u1 = single.macro()
     q1 = single.flux
+    f1 = single.lagrangian_force() if with_ib else None
 
     uid = rccl_unique_id(lib)
     out = [None] * n
@@ -74,7 +79,7 @@ def main():
                 lat.set_lagrangian(*pts(it))
             lat.step(1)
         rs, us = lat.macro()
-        out[r] = (xb, xc, rs, us, lat.flux)
+        out[r] = (xb, xc, rs, us, lat.flux, lat.lagrangian_force() if with_ib else None)  # collective
         gathered[r] = lat.gather_macro(0)  # collective output gather to rank 0
         lat.close()
 
@@ -103,7 +108,7 @@ def main():
             t.join()
     R = np.empty((ny, nx))
     U = np.empty((2, ny, nx))
-    for xb, xc, rs, us, _ in out:
+    for xb, xc, rs, us, _, _ in out:
         R[:, xb:xb + xc] = rs.reshape(ny, xc)
         U[:, :, xb:xb + xc] = us.reshape(2, ny, xc)
     R, U = R.ravel(), U.reshape(2, -1).ravel()
@@ -129,8 +134,12 @@ def main():
         rs_ok = rs_ok and abs(a[4] - b[2]) <= 1e-12 * max(abs(a[4]), 1e-300)
     rs_ok = rs_ok and (d_re == 0.0 if not with_ib else d_re <= 1e-12)
     ok = ok and g_ok and rs_ok
+    d_fs = 0.0
+    if with_ib:  # every rank reports the whole F_s (summed over the slabs that hold it)
+        d_fs = max(float(np.max(np.abs(o[5] - f1)) / np.max(np.abs(f1))) for o in out)
+        ok = ok and d_fs <= 1e-5
     print(json.dumps({"ok": bool(ok), "exact": exact, "d_rho": d_rho, "d_u": d_u, "d_flux": d_q, "n": n,
-                      "gather_ok": g_ok, "restart_ok": bool(rs_ok), "d_restart": d_re,
+                      "gather_ok": g_ok, "restart_ok": bool(rs_ok), "d_restart": d_re, "d_F_s": d_fs,
                       "with_ib": with_ib, "precision": prec}), flush=True)
     sys.exit(0 if ok else 1)
 

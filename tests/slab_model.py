@@ -1,5 +1,6 @@
 """Numpy model of the slab-decomposed step the HIP path implements (pull streaming with
-one-column halos, IB node values summed over slabs, spread clipped to owned columns).
+one-column halos; with IB a three-column halo so that every slab computes the nodes of the
+points that spread into it by itself; spread clipped to owned columns).
 TEST INFRASTRUCTURE: used by the CPU tests to check (a) that the pull form equals the
 reference's push streaming and (b) that the x-slab decomposition with the halo and IB
 exchange schedule of iblb_ctx.hip reproduces the single-domain reference step bit for bit.
@@ -90,22 +91,61 @@ class SlabRank:
         self.f = pull(self.g.reshape(self.ny, self.nc, 9), halo_left, halo_right).ravel()
         O.macro(self.f, self.u, self.rho, self.nc, self.ny)
 
+    # -- IB halo: columns -3..-1 and ncol..ncol+2 of g from the neighbours -------------------
+    def boundary_ext(self):
+        """(to the right neighbour, to the left neighbour): my last / first three columns of g
+        (ny, 3, 9).  The HIP path sends only the 21 planes of them that are read."""
+        g = self.g.reshape(self.ny, self.nc, 9)
+        return g[:, -3:, :].copy(), g[:, :3, :].copy()
+
+    def stream_macro_ext(self, left3, right3):
+        """Post-stream f and macro of the own columns (as stream_macro) plus rho, u_raw of
+        the node columns -2..ncol+1 (self.ext_rho / self.ext_u, column index + 2)."""
+        g = self.g.reshape(self.ny, self.nc, 9)
+        ext = np.concatenate([left3, g, right3], axis=1)          # columns -3 .. ncol+2
+        z = np.zeros((self.ny, 3))
+        fe = pull(ext, z, z)[:, 1:-1, :]                           # valid: columns -2 .. ncol+1
+        self.f = np.ascontiguousarray(fe[:, 2:2 + self.nc, :]).ravel()
+        self.O.macro(self.f, self.u, self.rho, self.nc, self.ny)
+        ne = self.nc + 4
+        self.ext_rho, self.ext_u = np.zeros(ne * self.ny), np.zeros(2 * ne * self.ny)
+        self.O.macro(np.ascontiguousarray(fe).ravel(), self.ext_u, self.ext_rho, ne, self.ny)
+
+    def processes(self, s, k) -> bool:
+        """Does point k spread into this slab (its 3x3 columns, clipped to the lattice)?"""
+        x0 = int(np.rint(np.float64(s[2 * k])))
+        return any(0 <= x < self.nx and self.xb <= x < self.xb + self.nc for x in (x0 - 1, x0, x0 + 1))
+
+    def owns(self, s, k) -> bool:
+        """The slab holding column min(x0, nx-1) reports F_s of point k (every point spreads
+        there, given the reference's invariant 0 <= x0 <= XDIM)."""
+        x = min(int(np.rint(np.float64(s[2 * k]))), self.nx - 1)
+        return self.xb <= x < self.xb + self.nc
+
     def node_values(self, s):
-        """(rho, u_x, u_y) at the 3x3 nodes of every point that this slab owns, zeros elsewhere."""
+        """(rho, u_x, u_y) at the 3x3 nodes of every point this slab processes, from the
+        node columns of the IB halo; zeros for the other points."""
         ns = s.size // 2
         nv = np.zeros((ns, 9, 3))
         size = self.nx * self.ny
+        ne = self.nc + 4
         for k in range(ns):
+            if not self.processes(s, k):
+                continue
             x0, y0 = int(np.rint(np.float64(s[2 * k]))), int(np.rint(np.float64(s[2 * k + 1])))
             for i in range(9):
                 j = (y0 + C_L[i, 1]) * self.nx + (x0 + C_L[i, 0])
                 if j < 0 or j >= size:
                     continue
                 xj, yj = j % self.nx, j // self.nx
-                xc = xj - self.xb
-                if 0 <= xc < self.nc:
-                    jl = yj * self.nc + xc
-                    nv[k, i] = (self.rho[jl], self.u[jl], self.u[self.n + jl])
+                xl = xj - self.xb       # flat-index node -> slab-local column, periodic
+                if xl < -2:
+                    xl += self.nx
+                elif xl > self.nc + 1:
+                    xl -= self.nx
+                assert -2 <= xl <= self.nc + 1
+                je = yj * ne + xl + 2
+                nv[k, i] = (self.ext_rho[je], self.ext_u[je], self.ext_u[ne * self.ny + je])
         return nv
 
     def interp(self, s, u_s, nv):

@@ -1,7 +1,8 @@
 """N>1 path on CPU: world_size 2 and 3 over torch.distributed (gloo) run the x-slab
 decomposition the HIP path uses — slab plan from cuda_iblb_11_amd.plan_slabs, halo planes
-{1,5,8} rightward / {3,6,7} leftward every step, IB node values summed over ranks, spread
-clipped to owned columns, flux owned by the slab holding column XDIM-5 — with the oracle
+{1,5,8} rightward / {3,6,7} leftward every step; with IB a three-column halo from which each
+rank computes the nodes of every point spreading into it (no collective), spread clipped to
+owned columns; flux owned by the slab holding column XDIM-5 — with the oracle
 kernels doing the per-cell arithmetic, and must reproduce the single-domain reference step
 bit for bit."""
 import os
@@ -17,6 +18,16 @@ def _free_port() -> int:
     port = s.getsockname()[1]
     s.close()
     return port
+
+
+def _points(it, nx, world):
+    from cuda_iblb_11_amd import workloads as W
+    from cuda_iblb_11_amd.lattice import plan_slabs
+    if world < 3:
+        x0, sway = plan_slabs(nx, world)[0][1] - 0.6, 1.5
+    else:
+        x0, sway = nx - 0.3, 0.5
+    return W.filament(it, n_points=30, x0=x0, y0=2.0, dy=1.0, U0=2e-3, period=20, sway=sway)
 
 
 def _worker(rank, world, port, nx, ny, steps, with_ib, out_dir):
@@ -41,35 +52,38 @@ def _worker(rank, world, port, nx, ny, steps, with_ib, out_dir):
     rk = SM.SlabRank(O, nx, ny, xb, xc, W.TAU, W.TAU2, split_state(rho, 1, nx, ny, xb, xc),
                      split_state(u, 2, nx, ny, xb, xc), body_force=bf)
     left, right = (rank - 1) % world, (rank + 1) % world
-    # the same points on every rank, straddling the edge between slab 0 and slab 1
-    x_edge = plan_slabs(nx, world)[0][1] - 0.6
-    pts = lambda it: W.filament(it, n_points=30, x0=x_edge, y0=2.0, dy=1.0, U0=2e-3, period=20, sway=1.5)
+    # the same points on every rank: straddling the edge between slab 0 and slab 1, or (3 ranks)
+    # at x = XDIM where the nodes wrap to column 0 of the next row
+    pts = lambda it: _points(it, nx, world)
     rk.collide()  # iteration 0's equilibrium + collision from rho^0, u^0, force^0
+    F_all = []
     for it in range(steps):
-        send_r, send_l = rk.boundary()
-        hl = torch.empty(ny, 3, dtype=torch.float64)
-        hr = torch.empty(ny, 3, dtype=torch.float64)
+        send_r, send_l = rk.boundary_ext() if with_ib else rk.boundary()
+        hl = torch.empty(send_r.shape, dtype=torch.float64)
+        hr = torch.empty(send_l.shape, dtype=torch.float64)
         reqs = [dist.isend(torch.from_numpy(send_r), right, tag=0), dist.isend(torch.from_numpy(send_l), left, tag=1),
                 dist.irecv(hl, left, tag=0), dist.irecv(hr, right, tag=1)]
         for r in reqs:
             r.wait()
-        rk.stream_macro(hl.numpy(), hr.numpy())
         if with_ib:
+            rk.stream_macro_ext(hl.numpy(), hr.numpy())
             s, us, eps = pts(it)
-            nv = torch.from_numpy(rk.node_values(s))
-            dist.all_reduce(nv)
-            F_s = rk.interp(s, us, nv.numpy())
+            F_s = rk.interp(s, us, rk.node_values(s))
             rk.spread(s, F_s, eps)
+            mine = np.array([rk.owns(s, k) for k in range(s.size // 2)])
+            F_all.append(np.where(np.repeat(mine, 2), F_s, np.float32(0)))
         else:
+            rk.stream_macro(hl.numpy(), hr.numpy())
             rk.no_ib()
         if it < steps - 1:
             rk.collide()
-    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), rho=rk.rho, u=rk.u, Q=rk.Q, xb=xb, xc=xc)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), rho=rk.rho, u=rk.u, Q=rk.Q, xb=xb, xc=xc,
+             F_s=np.array(F_all, dtype=np.float32))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,with_ib", [(2, False), (2, True), (3, False)])
+@pytest.mark.parametrize("world,with_ib", [(2, False), (2, True), (3, False), (3, True)])
 def test_slab_decomposition_gloo(tmp_path, oracle, world, with_ib):
     import torch.multiprocessing as mp
     nx, ny, steps = 30, 24 if not with_ib else 30, 12
@@ -86,12 +100,14 @@ def test_slab_decomposition_gloo(tmp_path, oracle, world, with_ib):
     from cuda_iblb_11_amd.lattice import plan_slabs
     rho, u = W.perturbed_state(nx, ny, 17)
     sim = oracle.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=(1e-6, 2e-7))
-    x_edge = plan_slabs(nx, world)[0][1] - 0.6
+    F_ref = []
     for it in range(steps):
         if with_ib:
-            s, us, eps = W.filament(it, n_points=30, x0=x_edge, y0=2.0, dy=1.0, U0=2e-3, period=20, sway=1.5)
+            s, us, eps = _points(it, nx, world)
             sim.set_lagrangian(s, us, eps)
         sim.step(1)
+        if with_ib:
+            F_ref.append(sim.F_s.copy())
     R = np.empty((ny, nx))
     U = np.empty((2, ny, nx))
     Q = 0.0
@@ -104,3 +120,6 @@ def test_slab_decomposition_gloo(tmp_path, oracle, world, with_ib):
     assert np.array_equal(R.ravel(), sim.rho)
     assert np.array_equal(U.reshape(2, -1).ravel(), sim.u)
     assert Q == sim.flux
+    if with_ib:  # every point's F_s reported by exactly one rank, equal to the reference's
+        F = sum(np.load(tmp_path / f"rank{r}.npz")["F_s"] for r in range(world))
+        assert np.array_equal(F, np.array(F_ref, dtype=np.float32))

@@ -181,7 +181,12 @@ def test_local_slab_group(gpu, oracle, nslab):
     from cuda_iblb_11_amd import workloads as W
     nx, ny = 90, 192
     rho, u = W.perturbed_state(nx, ny, 9)
-    pts = _filament_points(nx)
+    fil = _filament_points(nx)
+
+    def pts(it):  # plus a filament at x = XDIM whose nodes wrap to column 0 of the next row
+        a = fil(it)
+        b = W.filament(it, n_points=20, x0=nx - 0.3, y0=40.0, dy=1.0, U0=2e-3, period=40, sway=0.5)
+        return tuple(np.concatenate([p, q]) for p, q in zip(a, b))
     for with_ib in (False, True):
         single = gpu.Lattice(nx, ny, W.TAU, W.TAU2, body_force=(1e-6, 0.0), max_points=4096 if with_ib else 0)
         single.set_state(rho, u)
@@ -204,6 +209,8 @@ def test_local_slab_group(gpu, oracle, nslab):
         rg, ug = group.gather_macro()
         if with_ib:
             assert rel(rg, r1) <= 1e-13 and rel(ug, u1) <= 1e-12
+            # each point's F_s is reported by one slab (zeros elsewhere)
+            assert rel(sum(s.lagrangian_force() for s in slabs), single.lagrangian_force()) <= 1e-5
         else:
             assert np.array_equal(rg, r1) and np.array_equal(ug, u1)
         assert abs(group.flux - single.flux) <= 1e-12 * max(abs(single.flux), 1e-30)
@@ -362,3 +369,39 @@ def test_checkpoint_refuses_mismatch(gpu, tmp_path):
             other.load_checkpoint(str(tmp_path / "s.ck"))
     with pytest.raises(gpu.IblbError):
         a.load_checkpoint(str(tmp_path / "missing.ck"))
+
+
+@pytest.mark.parametrize("overlap", [1, 0])
+@pytest.mark.parametrize("with_ib", [False, True])
+def test_rccl_self_ring(gpu, monkeypatch, overlap, with_ib):
+    """The multi-slab schedule over REAL RCCL on one GPU: one rank that is its own left and
+    right neighbour (IBLB_RCCL_SELF=1) runs the comm-stream halo exchange, the interior /
+    boundary split, the node all-reduce and the output gather; it must equal the plain single
+    slab (bit-identical without IB)."""
+    from cuda_iblb_11_amd import workloads as W
+    monkeypatch.setenv("IBLB_RCCL_SELF", "1")
+    monkeypatch.setenv("IBLB_OVERLAP", str(overlap))
+    nx, ny, steps = 96, 200, 30
+    rho, u = W.perturbed_state(nx, ny, 5)
+    pts = lambda it: W.filament(it, n_points=40, x0=nx - 0.6, y0=1.0, U0=2e-3, period=30, sway=2.0)
+    kw = dict(body_force=(1e-6, 2e-7), max_points=64 if with_ib else 0)
+    ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)
+    ring = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)
+    ref.set_state(rho, u)
+    ring.set_state(rho, u)
+    ring.attach_rccl(gpu.rccl_unique_id(), 1, 0)
+    for it in range(steps):
+        if with_ib:
+            ref.set_lagrangian(*pts(it))
+            ring.set_lagrangian(*pts(it))
+        ref.step(1)
+        ring.step(1)
+    r1, u1 = ref.macro()
+    r2, u2 = ring.macro()
+    g2, gu2 = ring.gather_macro(0)
+    assert np.array_equal(g2, r2) and np.array_equal(gu2, u2)
+    if with_ib:
+        assert np.max(np.abs(r1 - r2)) <= 1e-13 and np.max(np.abs(u1 - u2)) <= 1e-13
+    else:
+        assert np.array_equal(r1, r2) and np.array_equal(u1, u2)
+    assert abs(ring.flux - ref.flux) <= 1e-13 * abs(ref.flux)
