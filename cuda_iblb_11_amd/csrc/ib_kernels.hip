@@ -38,7 +38,7 @@ __device__ __forceinline__ void spread_node(const Layout& L, int nx, int x_begin
     if (xc < 0 || xc >= L.ncol) return;
     const float del = d_delta(xs, ys, x, y);
     if (del == 0.f) return;
-    const long o = (long)xc * L.col + y;
+    const long o = (long)xc * L.rows + y;
     atomicAdd(fd + o, (double)(Fx * del) * 1. * (double)e);
     atomicAdd(fd + fplane + o, (double)(Fy * del) * 1. * (double)e);
     flags[(long)xc * nch + y / rows_per_chunk] = 1;
@@ -202,7 +202,7 @@ __global__ void pack_ib_halo_kernel(const T* __restrict__ g, Layout L, T* __rest
     const int d = send_slot_depth(s), k = send_slot_plane(right != 0, s);
     const int xc = right ? L.ncol - 1 - d : d;
     T* dst = right ? send_right : send_left;
-    dst[(long)s * L.col + y] = g[k * L.plane + (long)xc * L.col + y];
+    dst[(long)s * L.rows + y] = g[k * L.plane + (long)xc * L.col + y];
 }
 
 template <typename T>

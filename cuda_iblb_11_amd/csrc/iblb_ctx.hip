@@ -169,8 +169,8 @@ Halo<T> halo_of(iblb_ctx* c, int which) {
         }
     } else {
         for (int p = 0; p < 3; ++p) {
-            H.left[p] = (const T*)c->recv_left + p * L.col;
-            H.right[p] = (const T*)c->recv_right + p * L.col;
+            H.left[p] = (const T*)c->recv_left + p * L.rows;
+            H.right[p] = (const T*)c->recv_right + p * L.rows;
         }
     }
     return H;
@@ -179,8 +179,8 @@ Halo<T> halo_of(iblb_ctx* c, int which) {
 template <typename T>
 void send_ptrs(iblb_ctx* c, T* sl[3], T* sr[3]) {
     for (int p = 0; p < 3; ++p) {
-        sl[p] = single_slab(c) ? nullptr : (T*)c->send_left + p * c->L.col;
-        sr[p] = single_slab(c) ? nullptr : (T*)c->send_right + p * c->L.col;
+        sl[p] = single_slab(c) ? nullptr : (T*)c->send_left + p * c->L.rows;
+        sr[p] = single_slab(c) ? nullptr : (T*)c->send_right + p * c->L.rows;
     }
 }
 
@@ -234,6 +234,7 @@ int pack_ib(iblb_ctx* c, hipStream_t st) {
     return IBLB_OK;
 }
 int pack_ib_any(iblb_ctx* c, hipStream_t st) {
+    if (c->ncol < 3) return fail(c, IBLB_ERR_ARG, "immersed boundary across slabs needs >= 3 columns per slab");
     return c->prec == IBLB_PREC_F64 ? pack_ib<double>(c, st) : pack_ib<float>(c, st);
 }
 
@@ -243,7 +244,7 @@ int exchange_rccl(iblb_ctx* c, hipStream_t st, bool ib = false) {
     int rc;
     if (ib && (rc = pack_ib_any(c, st))) return rc;
     if ((rc = ev_begin(c, &ev, st))) return rc;
-    const size_t n = (size_t)(ib ? IB_HALO_SLOTS : HALO_SLOTS) * c->L.col;
+    const size_t n = (size_t)(ib ? IB_HALO_SLOTS : HALO_SLOTS) * c->L.rows;
     const ncclDataType_t dt = c->prec == IBLB_PREC_F64 ? ncclFloat64 : ncclFloat32;
     const int lr = (c->rank + c->nranks - 1) % c->nranks, rr = (c->rank + 1) % c->nranks;
     NCCL_TRY(c, ncclGroupStart());
@@ -259,7 +260,7 @@ int exchange_rccl(iblb_ctx* c, hipStream_t st, bool ib = false) {
 
 // local group: the neighbours' send buffers are complete (group_exchange packed them)
 int exchange_local(iblb_ctx* c, bool ib) {
-    const size_t bytes = (size_t)(ib ? IB_HALO_SLOTS : HALO_SLOTS) * c->L.col * c->esize;
+    const size_t bytes = (size_t)(ib ? IB_HALO_SLOTS : HALO_SLOTS) * c->L.rows * c->esize;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipMemcpyAsync(c->recv_left, c->left->send_right, bytes, hipMemcpyDefault, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->recv_right, c->right->send_left, bytes, hipMemcpyDefault, c->stream));
@@ -276,9 +277,9 @@ int pack_send(iblb_ctx* c) {
     for (int p = 0; p < 3; ++p) {
         const char* r = g + ((size_t)left_plane(p) * c->L.plane + (size_t)(c->ncol - 1) * c->L.col) * c->esize;
         const char* l = g + (size_t)right_plane(p) * c->L.plane * c->esize;
-        HIP_TRY(c, hipMemcpyAsync((char*)c->send_right + p * c->L.col * c->esize, r, n, hipMemcpyDeviceToDevice,
+        HIP_TRY(c, hipMemcpyAsync((char*)c->send_right + p * c->L.rows * c->esize, r, n, hipMemcpyDeviceToDevice,
                                   c->stream));
-        HIP_TRY(c, hipMemcpyAsync((char*)c->send_left + p * c->L.col * c->esize, l, n, hipMemcpyDeviceToDevice,
+        HIP_TRY(c, hipMemcpyAsync((char*)c->send_left + p * c->L.rows * c->esize, l, n, hipMemcpyDeviceToDevice,
                                   c->stream));
     }
     if (rccl_multi(c)) HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
@@ -605,29 +606,41 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(c, IBLB_ERR_HIP, "hipStreamCreate failed"));
 
-    // slab layout: column stride a multiple of one wave's rows, planes padded apart
-    const long col = (long)round_up((size_t)c->ny, (size_t)(64 * c->V));
-    // planes padded apart so the 9 read and 9 write streams do not start on the same HBM
-    // channel; a zero pad costs ~15 % (profiles/r01_tune_*.log); beyond that the choice is noise
-    const long pad = env_long("IBLB_PLANE_PAD", c->prec == IBLB_PREC_F64 ? 256 : 1024);
+    // slab layout: a column of a plane holds `rows` = ny rounded up to whole waves.
+    //  planar (default): g[k*plane + xc*rows + y], planes padded apart so the 9 read and 9
+    //    write streams do not start on the same HBM channel; a zero pad costs ~15 %
+    //    (profiles/r01_tune_*.log), beyond that the choice is noise
+    //  interleaved (IBLB_LAYOUT=1, experiment): g[xc*col + k*plane + y], the 9 planes of a
+    //    column adjacent (plane = rows + IBLB_PLANE_PAD, col = 9*plane + IBLB_COL_PAD)
+    const long rows = (long)round_up((size_t)c->ny, (size_t)(64 * c->V));
+    const bool interleaved = env_long("IBLB_LAYOUT", 0) == 1;
     c->L.ny = c->ny;
     c->L.ncol = c->ncol;
-    c->L.col = col;
-    c->L.plane = (long)c->ncol * col + pad;
-    c->fplane = (long)c->ncol * col;
+    c->L.rows = rows;
+    long buf;  // elements of one population buffer
+    if (interleaved) {
+        c->L.plane = rows + env_long("IBLB_PLANE_PAD", 0);
+        c->L.col = 9 * c->L.plane + env_long("IBLB_COL_PAD", 0);
+        buf = (long)c->ncol * c->L.col;
+    } else {
+        c->L.col = rows;
+        c->L.plane = (long)c->ncol * rows + env_long("IBLB_PLANE_PAD", c->prec == IBLB_PREC_F64 ? 256 : 1024);
+        buf = 9 * c->L.plane;
+    }
+    c->fplane = (long)c->ncol * rows;
     // buffer 1 starts `gap` elements after the end of buffer 0
     const long gap = env_long("IBLB_BUF_GAP", c->prec == IBLB_PREC_F64 ? 320 : 0);
-    const size_t gbytes = (size_t)(2 * 9 * c->L.plane + gap + 2 * GUARD) * c->esize;
+    const size_t gbytes = (size_t)(2 * buf + gap + 2 * GUARD) * c->esize;
     {
         int rc = alloc_zero(c, (void**)&c->g_alloc, gbytes);
         if (rc) return bail(rc);
         c->g[0] = c->g_alloc + GUARD * c->esize;
-        c->g[1] = c->g_alloc + (GUARD + 9 * c->L.plane + gap) * c->esize;
+        c->g[1] = c->g_alloc + (GUARD + buf + gap) * c->esize;
     }
-    // halo buffers: recv_left, recv_right, send_left, send_right; each 3 slots + guards
+    // halo buffers: recv_left, recv_right, send_left, send_right; each 3 (IB: 21) slots + guards
     {
         c->halo_slots = c->max_points > 0 ? IB_HALO_SLOTS : HALO_SLOTS;
-        const size_t slot = (size_t)(c->halo_slots * col + 2 * GUARD) * c->esize;
+        const size_t slot = (size_t)(c->halo_slots * rows + 2 * GUARD) * c->esize;
         int rc = alloc_zero(c, (void**)&c->halo_alloc, 4 * slot);
         if (rc) return bail(rc);
         c->recv_left = c->halo_alloc + 0 * slot + GUARD * c->esize;

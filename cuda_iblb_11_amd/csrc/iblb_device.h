@@ -44,8 +44,10 @@ __host__ __device__ constexpr int halo_slot(int k) {  // slot of plane k inside 
 struct Layout {
     int ny;      // lattice height Y
     int ncol;    // columns in this slab
-    long col;    // column stride (elements)
-    long plane;  // plane stride (elements)
+    long col;    // column stride of the populations (elements)
+    long plane;  // plane stride of the populations (elements)
+    long rows;   // ny rounded up to whole waves: one halo slot, the column stride of the
+                 // dense force and boot fields (plane stride fplane = ncol * rows)
 };
 
 // Pointers to the three halo planes of column -1 (left, planes 1,5,8) and column
@@ -137,8 +139,8 @@ struct IbHalo {
 template <typename T>
 __device__ __forceinline__ const T* ib_col(const T* __restrict__ g, const Layout& L, const IbHalo<T>& X, int xl,
                                            int k) {
-    if (xl < 0) return X.left + (long)ib_slot(true, -1 - xl, k) * L.col;
-    if (xl >= L.ncol) return X.right + (long)ib_slot(false, xl - L.ncol, k) * L.col;
+    if (xl < 0) return X.left + (long)ib_slot(true, -1 - xl, k) * L.rows;
+    if (xl >= L.ncol) return X.right + (long)ib_slot(false, xl - L.ncol, k) * L.rows;
     return g + k * L.plane + (long)xl * L.col;
 }
 

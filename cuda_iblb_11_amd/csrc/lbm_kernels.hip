@@ -174,8 +174,8 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
 #pragma unroll
     for (int e = 0; e < V; ++e) { fxv[e] = 0.; fyv[e] = 0.; }
     if (IB && has_f) {
-        double* fx = a.fdense + cb + y0;
-        double* fy = a.fdense + a.fplane + cb + y0;
+        double* fx = a.fdense + (long)xc * L.rows + y0;
+        double* fy = a.fdense + a.fplane + (long)xc * L.rows + y0;
 #pragma unroll
         for (int e = 0; e < V; ++e) { fxv[e] = fx[e]; fyv[e] = fy[e]; fx[e] = 0.; fy[e] = 0.; }
         if (lane == 0) a.flags[(long)xc * a.nch + ch] = 0;  // only this wave reads this flag
@@ -263,13 +263,13 @@ __global__ __launch_bounds__(256) void boot_kernel(const T* __restrict__ src, T*
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (long)L.ncol * L.ny) return;
     const int xc = (int)(idx / L.ny), y = (int)(idx - (long)xc * L.ny);
-    const long o = (long)xc * L.col + y;
+    const long o = (long)xc * L.col + y, of = (long)xc * L.rows + y;
     R f[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) f[i] = (R)src[i * L.plane + o];
-    const double rho = rho0[o];
-    const R ux = (R)u0[o], uy = (R)u0[fplane + o];
-    const R Fx = (R)(c.gx + (force0 ? force0[o] : 0.)), Fy = (R)(c.gy + (force0 ? force0[fplane + o] : 0.));
+    const double rho = rho0[of];
+    const R ux = (R)u0[of], uy = (R)u0[fplane + of];
+    const R Fx = (R)(c.gx + (force0 ? force0[of] : 0.)), Fy = (R)(c.gy + (force0 ? force0[fplane + of] : 0.));
     collide<R, DEV>(f, (R)rho, (R)(rho - 1.0), ux, uy, Fx, Fy, c);
 #pragma unroll
     for (int i = 0; i < 9; ++i) dst[i * L.plane + o] = (T)f[i];
@@ -310,7 +310,7 @@ __global__ void macro_out_kernel(const T* __restrict__ g, Layout L, Halo<T> H, c
     pull_cell<T>(g, L, H, xc, y, f);
     double r, mx, my;
     moments<double>(f, r, mx, my);
-    const long o = (long)xc * L.col + y;
+    const long o = (long)xc * L.rows + y;
     const double Fx = (fdense ? fdense[o] : 0.) + gx;
     const double Fy = (fdense ? fdense[fplane + o] : 0.) + gy;
     if (rho_out) rho_out[idx] = r;
@@ -362,7 +362,7 @@ __global__ void flux_kernel(const T* __restrict__ g, Layout L, Halo<T> H, const 
         pull_cell<T>(g, L, H, xc, y, f);
         double r, mx, my;
         moments<double>(f, r, mx, my);
-        const long o = (long)xc * L.col + y;
+        const long o = (long)xc * L.rows + y;
         const double Fx = (fdense ? fdense[o] : 0.) + gx;
         q += ((mx + 0.5 * Fx) / r) / flux_norm;
     }
@@ -399,7 +399,7 @@ __global__ void field_in_kernel(const double* __restrict__ ref, double* __restri
     const long N = (long)L.ncol * L.ny;
     if (idx >= N) return;
     const int y = (int)(idx / L.ncol), xc = (int)(idx - (long)y * L.ncol);
-    for (int a = 0; a < ncomp; ++a) lay[a * fplane + (long)xc * L.col + y] = ref[a * N + idx];
+    for (int a = 0; a < ncomp; ++a) lay[a * fplane + (long)xc * L.rows + y] = ref[a * N + idx];
 }
 
 __global__ void field_out_kernel(const double* __restrict__ lay, double* __restrict__ ref, Layout L, int ncomp,
@@ -409,7 +409,7 @@ __global__ void field_out_kernel(const double* __restrict__ lay, double* __restr
     if (idx >= N) return;
     const int y = (int)(idx / L.ncol), xc = (int)(idx - (long)y * L.ncol);
     for (int a = 0; a < ncomp; ++a)
-        ref[a * N + idx] = (lay ? lay[a * fplane + (long)xc * L.col + y] : 0.) + (a == 0 ? add0 : add1);
+        ref[a * N + idx] = (lay ? lay[a * fplane + (long)xc * L.rows + y] : 0.) + (a == 0 ? add0 : add1);
 }
 
 hipError_t launch_field_in(const double* ref, double* lay, Layout L, int ncomp, long fplane, hipStream_t s) {

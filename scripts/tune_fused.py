@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--variants", default="0,1,2,3,4,5,6,7")
     ap.add_argument("--pads", default="")
     ap.add_argument("--gaps", default="", help="IBLB_BUF_GAP values, crossed with --pads")
+    ap.add_argument("--envs", default="", help="';'-separated environment sets, e.g. "
+                    "'IBLB_FUSED_VARIANT=5;IBLB_FUSED_VARIANT=5 IBLB_LAYOUT=1 IBLB_COL_PAD=64' (overrides the rest)")
     a = ap.parse_args()
     import cuda_iblb_11_amd as P
     from cuda_iblb_11_amd import workloads as W
@@ -34,20 +36,31 @@ def main():
     if a.pads:
         gaps = [int(g) for g in a.gaps.split(",")] if a.gaps else [None]
         combos = [(int(v), int(p), g) for v in a.variants.split(",") for p in a.pads.split(",") for g in gaps]
-    ctxs = []
+    sets = []
     for v, pad, gap in combos:
-        os.environ["IBLB_FUSED_VARIANT"] = str(v)
-        for name, val in (("IBLB_PLANE_PAD", pad), ("IBLB_BUF_GAP", gap)):
-            if val is None:
-                os.environ.pop(name, None)
-            else:
-                os.environ[name] = str(val)
+        e = {"IBLB_FUSED_VARIANT": str(v)}
+        if pad is not None:
+            e["IBLB_PLANE_PAD"] = str(pad)
+        if gap is not None:
+            e["IBLB_BUF_GAP"] = str(gap)
+        sets.append(((v, pad, gap), e))
+    if a.envs:
+        sets = []
+        for grp in a.envs.split(";"):
+            e = dict(kv.split("=") for kv in grp.split())
+            sets.append((grp, e))
+    names = sorted({k for _, e in sets for k in e} | {"IBLB_FUSED_VARIANT", "IBLB_PLANE_PAD", "IBLB_BUF_GAP"})
+    ctxs = []
+    for key, e in sets:
+        for name in names:
+            os.environ.pop(name, None)
+        os.environ.update(e)
         lat = P.Lattice(a.nx, a.ny, W.TAU, W.TAU2, precision=a.precision, body_force=W.BODY_FORCE)
         lat.set_state(rho, u)
         lat.step(10)
         lat.set_profiling(True)
-        ctxs.append(((v, pad, gap), lat))
-    for name in ("IBLB_FUSED_VARIANT", "IBLB_PLANE_PAD", "IBLB_BUF_GAP"):
+        ctxs.append((key, lat))
+    for name in names:
         os.environ.pop(name, None)
     res = {k: [] for k, _ in ctxs}
     for r in range(a.rounds):
@@ -64,7 +77,7 @@ def main():
         ms = np.array(res[k])
         r_, u_ = lat.macro()
         same = bool(np.array_equal(r_, ref_rho) and np.array_equal(u_, ref_u))
-        row = {"variant": k[0], "pad": k[1], "gap": k[2], "median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
+        row = {"config": k, "median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
                "tbps_median": bpc * cells / (np.median(ms) * 1e-3) / 1e12, "bitwise_equal_to_first": same}
         print(json.dumps(row), flush=True)
 

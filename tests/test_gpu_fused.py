@@ -405,3 +405,24 @@ def test_rccl_self_ring(gpu, monkeypatch, overlap, with_ib):
     else:
         assert np.array_equal(r1, r2) and np.array_equal(u1, u2)
     assert abs(ring.flux - ref.flux) <= 1e-13 * abs(ref.flux)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_interleaved_layout_identical(gpu, monkeypatch, precision):
+    """IBLB_LAYOUT=1 (the 9 planes of a column adjacent) is a pure storage permutation: same
+    fields bit for bit as the planar layout, IB and readers included."""
+    from cuda_iblb_11_amd import workloads as W
+    nx, ny = 70, 150
+    rho, u = W.perturbed_state(nx, ny, 3)
+    pts = _filament_points(nx)
+    out = []
+    for layout in ("0", "1"):
+        monkeypatch.setenv("IBLB_LAYOUT", layout)
+        lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 0.0), max_points=64)
+        lat.set_state(rho, u)
+        for it in range(20):
+            lat.set_lagrangian(*pts(it))
+            lat.step(1)
+        out.append((*lat.macro(), lat.populations(), lat.flux))
+    (r0, u0, f0, q0), (r1, u1, f1, q1) = out
+    assert rel(r1, r0) <= 1e-14 and rel(u1, u0) <= 1e-13 and rel(f1, f0) <= 1e-14 and abs(q1 - q0) <= 1e-13 * abs(q0)
