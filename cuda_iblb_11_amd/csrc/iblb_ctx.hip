@@ -1145,7 +1145,27 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         c->slab_count.assign(1, c->ncol);
     }
     if (rccl_multi(c)) {
-        HIP_TRY(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+        // The halo's RCCL kernels run beside the interior collide, which fills every CU: give
+        // the comm stream the highest priority (its workgroups go first as CUs free up) and,
+        // optionally, keep IBLB_RESERVE_CUS compute units free of the collide for them.
+        const long reserve = env_long("IBLB_RESERVE_CUS", 0);
+        if (reserve > 0) {
+            hipDeviceProp_t prop;
+            HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
+            const int ncu = prop.multiProcessorCount;
+            if (reserve >= ncu) return fail(c, IBLB_ERR_ARG, "IBLB_RESERVE_CUS exceeds the compute units");
+            std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+            for (int i = 0; i < ncu - (int)reserve; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+            hipStream_t masked = nullptr;
+            HIP_TRY(c, hipExtStreamCreateWithCUMask(&masked, (uint32_t)mask.size(), mask.data()));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            (void)hipStreamDestroy(c->stream);
+            c->stream = masked;
+        }
+        int prio_lo = 0, prio_hi = 0;
+        HIP_TRY(c, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        const int prio = env_long("IBLB_COMM_PRIORITY", 1) != 0 ? prio_hi : prio_lo;
+        HIP_TRY(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
