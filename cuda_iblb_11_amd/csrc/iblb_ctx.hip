@@ -109,8 +109,8 @@ struct iblb_ctx {
     bool self_ring = false;  // one rank that is its own neighbour over RCCL (IBLB_RCCL_SELF, rehearsal)
     std::vector<int> slab_begin, slab_count;  // every rank's columns (RCCL group)
     hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with the interior
-    hipEvent_t ev_bnd = nullptr;        // boundary columns + send buffers of the state written
-    hipEvent_t ev_comm = nullptr;       // halo of the state received
+    hipEvent_t ev_bnd = nullptr;  // boundary columns + send buffers of the state written (either stream)
+    hipEvent_t ev_int = nullptr;  // compute-stream work of the last step done
     bool overlap = true;
     // profiling
     bool prof = false;
@@ -282,7 +282,11 @@ int pack_send(iblb_ctx* c) {
         HIP_TRY(c, hipMemcpyAsync((char*)c->send_left + p * c->L.rows * c->esize, l, n, hipMemcpyDeviceToDevice,
                                   c->stream));
     }
-    if (rccl_multi(c)) HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+    if (rccl_multi(c)) {
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+    }
     return IBLB_OK;
 }
 
@@ -350,7 +354,8 @@ int launch_boot_step(iblb_ctx* c) {
 }
 
 template <typename T>
-int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, bool timed = true) {
+int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, bool timed = true,
+                      hipStream_t st = nullptr) {
     FusedArgs<T> a;
     a.src = gptr<T>(c, c->cur);
     a.dst = gptr<T>(c, 1 - c->cur);
@@ -374,7 +379,7 @@ int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, b
     size_t ev = 0;
     int rc = timed ? ev_begin(c, &ev) : IBLB_OK;
     if (rc) return rc;
-    HIP_TRY(c, launch_fused<T>(a, c->stream));
+    HIP_TRY(c, launch_fused<T>(a, st ? st : c->stream));
     return timed ? ev_end(c, ev, EV_FUSED, (long long)ncols * c->ny) : IBLB_OK;
 }
 
@@ -393,19 +398,30 @@ void after_step(iblb_ctx* c) {
     c->ib_state = ib_active(c) ? IB_PENDING : IB_NONE;
 }
 
-// RCCL slab, no IB force owed: exchange the boundary planes of the previous step on the
-// comm stream while the interior columns collide, then the two boundary columns.
+// RCCL slab, no IB force owed.  Step t on two streams:
+//   comm:    exchange(t) [send buffers of g^{t-1}] -> wait int(t-1) -> boundary columns(t) -> ev_bnd
+//   compute: (waited for ev_bnd = boundary(t-1) in step_one) -> interior columns(t) -> ev_int
+// The interior needs nothing from the exchange, so the halo and the two boundary columns run
+// beside it (on the CUs the collide leaves free, IBLB_RESERVE_CUS): the step costs the interior
+// launch as long as exchange + boundary are shorter.  boundary(t) waits for interior(t-1): it
+// reads columns 1 and ncol-2 of g^{t-1} and overwrites columns of the buffer interior(t-1) read.
 template <typename T>
 int overlapped_step(iblb_ctx* c) {
-    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     int rc = exchange_rccl(c, c->comm_stream);
     if (rc) return rc;
-    HIP_TRY(c, hipEventRecord(c->ev_comm, c->comm_stream));
+    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_int, 0));
+    if ((rc = launch_fused_step<T>(c, 0, 2, c->ncol - 1, false, c->comm_stream))) return rc;
+    HIP_TRY(c, hipEventRecord(c->ev_bnd, c->comm_stream));
     if ((rc = launch_fused_step<T>(c, 1, c->ncol - 2))) return rc;
-    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_comm, 0));
-    if ((rc = launch_fused_step<T>(c, 0, 2, c->ncol - 1, false))) return rc;
-    HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
     after_step(c);
+    return IBLB_OK;
+}
+
+// Compute stream after the boundary columns of the current state (they may have been written
+// on the comm stream by an overlapped step).
+int join_comm(iblb_ctx* c) {
+    if (c->comm_stream) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
     return IBLB_OK;
 }
 
@@ -421,7 +437,11 @@ int advance(iblb_ctx* c) {
         rc = f64 ? launch_fused_step<double>(c, 0, c->ncol) : launch_fused_step<float>(c, 0, c->ncol);
         if (rc) return rc;
     }
-    if (rccl_multi(c)) HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+    if (rccl_multi(c)) {  // the whole state was written on the compute stream
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+    }
     after_step(c);
     return IBLB_OK;
 }
@@ -447,7 +467,8 @@ int run_cilia(iblb_ctx* c) {
 }
 
 int step_one(iblb_ctx* c) {
-    int rc;
+    int rc = join_comm(c);
+    if (rc) return rc;
     if (c->cilia_on) {
         if (c->phase == PH_RUN) {
             if ((rc = ensure_halo(c))) return rc;
@@ -492,6 +513,7 @@ int prepare_read(iblb_ctx* c) {
     int rc = check_ready(c);
     if (rc) return rc;
     if (c->phase != PH_RUN) return IBLB_OK;
+    if ((rc = join_comm(c))) return rc;
     if (c->transport == TR_LOCAL) {
         if (!c->halo_valid || c->ib_state == IB_PENDING)
             return fail(c, IBLB_ERR_STATE, "local group state not prepared (use iblb_group_step)");
@@ -607,24 +629,26 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
         return bail(fail(c, IBLB_ERR_HIP, "hipStreamCreate failed"));
 
     // slab layout: a column of a plane holds `rows` = ny rounded up to whole waves.
-    //  planar (default): g[k*plane + xc*rows + y], planes padded apart so the 9 read and 9
-    //    write streams do not start on the same HBM channel; a zero pad costs ~15 %
-    //    (profiles/r01_tune_*.log), beyond that the choice is noise
-    //  interleaved (IBLB_LAYOUT=1, experiment): g[xc*col + k*plane + y], the 9 planes of a
-    //    column adjacent (plane = rows + IBLB_PLANE_PAD, col = 9*plane + IBLB_COL_PAD)
+    //  interleaved (f64 default, IBLB_LAYOUT=1): g[xc*col + k*plane + y], the 9 planes of a
+    //    column adjacent (plane = rows + IBLB_PLANE_PAD, col = 9*plane + IBLB_COL_PAD);
+    //    4096^2 f64: 0.398 ms vs 0.425 ms planar (profiles/r01d_tune_layout_f64.log)
+    //  planar (f32 default, IBLB_LAYOUT=0): g[k*plane + xc*rows + y], planes padded apart so
+    //    the 9 read and 9 write streams do not start on the same HBM channel (a zero pad costs
+    //    ~15 %, profiles/r01_tune_*.log); f32 interleaved is within 1 % of it
+    const bool f64 = c->prec == IBLB_PREC_F64;
     const long rows = (long)round_up((size_t)c->ny, (size_t)(64 * c->V));
-    const bool interleaved = env_long("IBLB_LAYOUT", 0) == 1;
+    const bool interleaved = env_long("IBLB_LAYOUT", f64 ? 1 : 0) == 1;
     c->L.ny = c->ny;
     c->L.ncol = c->ncol;
     c->L.rows = rows;
     long buf;  // elements of one population buffer
     if (interleaved) {
         c->L.plane = rows + env_long("IBLB_PLANE_PAD", 0);
-        c->L.col = 9 * c->L.plane + env_long("IBLB_COL_PAD", 0);
+        c->L.col = 9 * c->L.plane + env_long("IBLB_COL_PAD", 64);
         buf = (long)c->ncol * c->L.col;
     } else {
         c->L.col = rows;
-        c->L.plane = (long)c->ncol * rows + env_long("IBLB_PLANE_PAD", c->prec == IBLB_PREC_F64 ? 256 : 1024);
+        c->L.plane = (long)c->ncol * rows + env_long("IBLB_PLANE_PAD", f64 ? 256 : 1024);
         buf = 9 * c->L.plane;
     }
     c->fplane = (long)c->ncol * rows;
@@ -672,7 +696,7 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
-    if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
+    if (c->ev_int) (void)hipEventDestroy(c->ev_int);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->g_alloc) (void)hipFree(c->g_alloc);
     void* bufs[] = {c->cil_samples, c->cil_lasts, c->cil_bpoints,
@@ -1154,8 +1178,16 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
             HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
             const int ncu = prop.multiProcessorCount;
             if (reserve >= ncu) return fail(c, IBLB_ERR_ARG, "IBLB_RESERVE_CUS exceeds the compute units");
+            // reserved: CUs ncu-1, ncu-1-stride, ... (stride 32 spreads them over the XCDs if the
+            // mask numbers CUs XCD by XCD)
+            const long stride = std::max(1L, env_long("IBLB_RESERVE_STRIDE", 1));
             std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-            for (int i = 0; i < ncu - (int)reserve; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+            for (int i = 0; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+            for (long k = 0; k < reserve; ++k) {
+                const long i = ncu - 1 - k * stride;
+                if (i < 0) return fail(c, IBLB_ERR_ARG, "IBLB_RESERVE_CUS x IBLB_RESERVE_STRIDE exceeds the CUs");
+                mask[(size_t)i / 32] &= ~(1u << (i % 32));
+            }
             hipStream_t masked = nullptr;
             HIP_TRY(c, hipExtStreamCreateWithCUMask(&masked, (uint32_t)mask.size(), mask.data()));
             HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1167,8 +1199,9 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         const int prio = env_long("IBLB_COMM_PRIORITY", 1) != 0 ? prio_hi : prio_lo;
         HIP_TRY(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_int, hipEventDisableTiming));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
     }
     c->halo_valid = false;
