@@ -112,12 +112,6 @@ struct iblb_ctx {
     hipEvent_t ev_bnd = nullptr;  // boundary columns + send buffers of the state written (either stream)
     hipEvent_t ev_int = nullptr;  // compute-stream work of the last step done
     bool overlap = true;
-    // captured multi-step replay of the overlapped schedule (host cost of RCCL + launches paid
-    // once per GRAPH_STEPS steps); rebuilt when the starting buffer changes
-    int graph_steps = 0;  // 0 = off (IBLB_GRAPH_STEPS, default 16 for RCCL groups)
-    hipGraphExec_t graph_exec = nullptr;
-    int graph_cur = -1;
-    hipEvent_t ev_fork = nullptr;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -431,93 +425,6 @@ int join_comm(iblb_ctx* c) {
     return IBLB_OK;
 }
 
-// graph_steps overlapped steps as one captured graph (both streams, RCCL calls included).
-// Inside the capture the comm stream forks from the compute stream and joins it at the end, so a
-// replay starts after all earlier work and ends with every branch done.  graph_steps is even:
-// the buffers are back where they started and one graph serves every replay.
-template <typename T>
-int build_graph(iblb_ctx* c) {
-    if (c->graph_exec) {
-        (void)hipGraphExecDestroy(c->graph_exec);
-        c->graph_exec = nullptr;
-    }
-    if (!c->ev_fork) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-    const int cur0 = c->cur;
-    const long long t0 = c->t;
-    HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    int rc = IBLB_OK;
-    hipGraph_t graph = nullptr;
-    auto body = [&]() -> int {
-        HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
-        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
-        for (int i = 0; i < c->graph_steps; ++i) {
-            if (i > 0) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));  // boundary(t-1)
-            int r = exchange_rccl(c, c->comm_stream);
-            if (r) return r;
-            if (i > 0) HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_int, 0));  // interior(t-1)
-            if ((r = launch_fused_step<T>(c, 0, 2, c->ncol - 1, false, c->comm_stream))) return r;
-            HIP_TRY(c, hipEventRecord(c->ev_bnd, c->comm_stream));
-            if ((r = launch_fused_step<T>(c, 1, c->ncol - 2, 1, false))) return r;
-            HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
-            c->cur = 1 - c->cur;
-            c->halo_valid = false;
-        }
-        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));  // join the comm branch
-        return IBLB_OK;
-    };
-    rc = body();
-    const hipError_t e = hipStreamEndCapture(c->stream, &graph);  // always end the capture
-    c->cur = cur0;
-    c->t = t0;
-    if (rc) {
-        if (graph) (void)hipGraphDestroy(graph);
-        return rc;
-    }
-    if (e != hipSuccess) return hip_fail(c, e, "hipStreamEndCapture");
-    const hipError_t ei = hipGraphInstantiate(&c->graph_exec, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    if (ei != hipSuccess) {
-        c->graph_exec = nullptr;
-        return hip_fail(c, ei, "hipGraphInstantiate");
-    }
-    c->graph_cur = cur0;
-    return IBLB_OK;
-}
-
-// Can the next graph_steps steps replay the captured overlapped schedule?
-bool graph_ready(const iblb_ctx* c) {
-    return c->graph_steps > 0 && c->phase == PH_RUN && c->transport == TR_RCCL && c->comm_stream && c->overlap &&
-           !c->prof && !c->cilia_on && !ib_active(c) && c->ncol >= 3;
-}
-
-int step_one(iblb_ctx* c);
-
-int graph_run(iblb_ctx* c) {
-    if (!c->graph_exec || c->graph_cur != c->cur) {
-        int rc = c->prec == IBLB_PREC_F64 ? build_graph<double>(c) : build_graph<float>(c);
-        if (rc) {  // capture refused (e.g. by the RCCL build): stay on the eager schedule
-            std::fprintf(stderr, "iblb: graph capture of the slab schedule failed (%s); stepping eagerly\n",
-                         c->err.c_str());
-            (void)hipGetLastError();
-            c->graph_steps = 0;
-            c->err.clear();
-            return step_one(c);
-        }
-    }
-    int rc = join_comm(c);
-    if (rc) return rc;
-    HIP_TRY(c, hipGraphLaunch(c->graph_exec, c->stream));
-    // everything of the replay is ordered before later work on the compute stream; make the
-    // events say so for the eager schedule
-    HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
-    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
-    c->t += c->graph_steps;  // cur is unchanged (even step count)
-    c->halo_valid = false;
-    c->ib_state = IB_NONE;
-    return IBLB_OK;
-}
-
 // One reference iteration for a context whose halo (if any) and force^t are in place.
 int advance(iblb_ctx* c) {
     int rc;
@@ -700,9 +607,10 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->nch = chunks_per_column(c->ny, c->V);
     c->device = cfg->device;
     c->max_points = cfg->max_points;
-    // collide-stream variant measured fastest on MI355X (scripts/tune_fused.py, profiles/):
-    // f64 = DPP row shift + nontemporal stores (5), f32 = nontemporal loads (2)
-    c->variant = (int)env_long("IBLB_FUSED_VARIANT", c->prec == IBLB_PREC_F64 ? 5 : 2);
+    // collide-stream variant measured fastest on MI355X (scripts/tune_fused.py, profiles/) with
+    // the interleaved layout: f64 = DPP row shift + nontemporal stores (5), f32 = nontemporal
+    // loads and stores (3; 0.193 ms vs 0.218 ms planar variant 2, profiles/r01e_tune_f32.log)
+    c->variant = (int)env_long("IBLB_FUSED_VARIANT", c->prec == IBLB_PREC_F64 ? 5 : 3);
     if (c->cfg.flux_column < 0) c->cfg.flux_column = c->nx - 5;
 
     const double tau = cfg->tau, tau2 = cfg->tau2, cs = 0.57735;
@@ -722,22 +630,22 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
         return bail(fail(c, IBLB_ERR_HIP, "hipStreamCreate failed"));
 
     // slab layout: a column of a plane holds `rows` = ny rounded up to whole waves.
-    //  interleaved (f64 default, IBLB_LAYOUT=1): g[xc*col + k*plane + y], the 9 planes of a
+    //  interleaved (default, IBLB_LAYOUT=1): g[xc*col + k*plane + y], the 9 planes of a
     //    column adjacent (plane = rows + IBLB_PLANE_PAD, col = 9*plane + IBLB_COL_PAD);
     //    4096^2 f64: 0.398 ms vs 0.425 ms planar (profiles/r01d_tune_layout_f64.log)
-    //  planar (f32 default, IBLB_LAYOUT=0): g[k*plane + xc*rows + y], planes padded apart so
-    //    the 9 read and 9 write streams do not start on the same HBM channel (a zero pad costs
-    //    ~15 %, profiles/r01_tune_*.log); f32 interleaved is within 1 % of it
+    //  planar (IBLB_LAYOUT=0): g[k*plane + xc*rows + y], planes padded apart so the 9 read and
+    //    9 write streams do not start on the same HBM channel (a zero pad costs ~15 %,
+    //    profiles/r01_tune_*.log)
     const bool f64 = c->prec == IBLB_PREC_F64;
     const long rows = (long)round_up((size_t)c->ny, (size_t)(64 * c->V));
-    const bool interleaved = env_long("IBLB_LAYOUT", f64 ? 1 : 0) == 1;
+    const bool interleaved = env_long("IBLB_LAYOUT", 1) == 1;
     c->L.ny = c->ny;
     c->L.ncol = c->ncol;
     c->L.rows = rows;
     long buf;  // elements of one population buffer
     if (interleaved) {
         c->L.plane = rows + env_long("IBLB_PLANE_PAD", 0);
-        c->L.col = 9 * c->L.plane + env_long("IBLB_COL_PAD", 64);
+        c->L.col = 9 * c->L.plane + env_long("IBLB_COL_PAD", f64 ? 64 : 0);
         buf = (long)c->ncol * c->L.col;
     } else {
         c->L.col = rows;
@@ -790,8 +698,6 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
     if (c->ev_int) (void)hipEventDestroy(c->ev_int);
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->g_alloc) (void)hipFree(c->g_alloc);
     void* bufs[] = {c->cil_samples, c->cil_lasts, c->cil_bpoints,
@@ -962,16 +868,8 @@ int iblb_step(iblb_ctx* c, int nsteps) {
     int rc = check_ready(c);
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
-    for (int s = 0; s < nsteps;) {
-        if (graph_ready(c) && nsteps - s >= c->graph_steps) {
-            const long long t0 = c->t;
-            if ((rc = graph_run(c))) return rc;
-            s += (int)(c->t - t0);  // graph_steps, or 1 after a refused capture
-        } else {
-            if ((rc = step_one(c))) return rc;
-            ++s;
-        }
-    }
+    for (int s = 0; s < nsteps; ++s)
+        if ((rc = step_one(c))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return IBLB_OK;
 }
@@ -1275,7 +1173,9 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         // The halo's RCCL kernels run beside the interior collide, which fills every CU: give
         // the comm stream the highest priority (its workgroups go first as CUs free up) and,
         // optionally, keep IBLB_RESERVE_CUS compute units free of the collide for them.
-        const long reserve = env_long("IBLB_RESERVE_CUS", 0);
+        // 8 reserved CUs: 512 x 4096 f64 slab step 0.070 ms vs 0.165 ms without (self-ring
+        // rehearsal, profiles/r01e_gap_probe.txt); 4 or 16 are within 1 %
+        const long reserve = env_long("IBLB_RESERVE_CUS", 8);
         if (reserve > 0) {
             hipDeviceProp_t prop;
             HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
@@ -1306,7 +1206,6 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
-        c->graph_steps = (int)(env_long("IBLB_GRAPH_STEPS", 16) / 2 * 2);
     }
     c->halo_valid = false;
     int rc = pack_send(c);  // a restored state has no send buffers yet

@@ -15,8 +15,7 @@ for nx in 4096 1024 512; do
   row "plain $nx" "$OUT/b_${nx}.json"
 done
 for nx in 1024 512; do
-  for cfg in "IBLB_RESERVE_CUS=8 IBLB_GRAPH_STEPS=0" "IBLB_RESERVE_CUS=8" "IBLB_RESERVE_CUS=4" "IBLB_RESERVE_CUS=16" \
-             "IBLB_RESERVE_CUS=8 IBLB_GRAPH_STEPS=64" "IBLB_RESERVE_CUS=0" "IBLB_OVERLAP=0 IBLB_RESERVE_CUS=8"; do
+  for cfg in "IBLB_RESERVE_CUS=8" "IBLB_RESERVE_CUS=4" "IBLB_RESERVE_CUS=0" "IBLB_OVERLAP=0"; do
     tag=$(echo "$cfg" | tr '= ' '_-')
     env $cfg timeout -k 10 200 python bench.py --nx $nx --ny 4096 --steps 400 --warmup 40 --no-cpu-baseline \
       --no-profile-events --rccl-self > "$OUT/s_${nx}_${tag}.json" 2> "$OUT/s_${nx}_${tag}.err" \

@@ -23,8 +23,6 @@ from cuda_iblb_11_amd.lattice import Lattice, plan_slabs, rccl_unique_id, split_
 
 
 def main():
-    # the in-process RCCL stand-in synchronises on the host: it cannot be captured in a graph
-    os.environ["IBLB_GRAPH_STEPS"] = "0"
     n, nx, ny, steps, with_ib, prec = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]),
                                         sys.argv[5] == "1", sys.argv[6])
     lib = L.load_from(os.path.join(HERE, "libiblb_mockrccl.so"))
