@@ -15,11 +15,15 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/iblb.h"
@@ -112,6 +116,22 @@ struct iblb_ctx {
     hipEvent_t ev_bnd = nullptr;  // boundary columns + send buffers of the state written (either stream)
     hipEvent_t ev_int = nullptr;  // compute-stream work of the last step done
     bool overlap = true;
+    // A second host thread issues the comm-stream half of a batch of overlapped steps (RCCL
+    // group, boundary launch), the caller's thread the interior launches (IBLB_COMM_THREAD=0:
+    // one thread issues both).  Host counters order the event records and waits.
+    struct CommThread {
+        std::thread thr;
+        std::mutex mu;
+        std::condition_variable cv;
+        bool stop = false;
+        long long t0 = 0, n = 0, gen = 0;   // current batch: steps [t0, t0+n), generation
+        int cur0 = 0;
+        std::atomic<long long> bnd_issued{0}, int_issued{0};  // last step whose record is issued
+        std::atomic<int> err{0};
+        hipEvent_t ev_b[2] = {nullptr, nullptr};  // boundary(s) done, by step parity
+        hipEvent_t ev_i[2] = {nullptr, nullptr};  // interior(s) done
+    };
+    CommThread* ct = nullptr;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -258,6 +278,20 @@ int exchange_rccl(iblb_ctx* c, hipStream_t st, bool ib = false) {
     return ev_end(c, ev, EV_HALO, 0, st);
 }
 
+// the streaming halo exchange as the comm thread issues it (no profiling, no context state)
+int exchange_rccl_raw(iblb_ctx* c, hipStream_t st) {
+    const size_t n = (size_t)HALO_SLOTS * c->L.rows;
+    const ncclDataType_t dt = c->prec == IBLB_PREC_F64 ? ncclFloat64 : ncclFloat32;
+    const int lr = (c->rank + c->nranks - 1) % c->nranks, rr = (c->rank + 1) % c->nranks;
+    NCCL_TRY(c, ncclGroupStart());
+    NCCL_TRY(c, ncclSend(c->send_right, n, dt, rr, c->comm, st));
+    NCCL_TRY(c, ncclSend(c->send_left, n, dt, lr, c->comm, st));
+    NCCL_TRY(c, ncclRecv(c->recv_left, n, dt, lr, c->comm, st));
+    NCCL_TRY(c, ncclRecv(c->recv_right, n, dt, rr, c->comm, st));
+    NCCL_TRY(c, ncclGroupEnd());
+    return IBLB_OK;
+}
+
 // local group: the neighbours' send buffers are complete (group_exchange packed them)
 int exchange_local(iblb_ctx* c, bool ib) {
     const size_t bytes = (size_t)(ib ? IB_HALO_SLOTS : HALO_SLOTS) * c->L.rows * c->esize;
@@ -354,13 +388,12 @@ int launch_boot_step(iblb_ctx* c) {
 }
 
 template <typename T>
-int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, bool timed = true,
-                      hipStream_t st = nullptr) {
+int launch_fused_at(iblb_ctx* c, int cur, int col_begin, int ncols, int col_step, bool timed, hipStream_t st) {
     FusedArgs<T> a;
-    a.src = gptr<T>(c, c->cur);
-    a.dst = gptr<T>(c, 1 - c->cur);
+    a.src = gptr<T>(c, cur);
+    a.dst = gptr<T>(c, 1 - cur);
     a.L = c->L;
-    a.H = halo_of<T>(c, c->cur);
+    a.H = halo_of<T>(c, cur);
     send_ptrs<T>(c, a.send_left, a.send_right);
     a.col_begin = col_begin;
     a.col_step = col_step;
@@ -381,6 +414,12 @@ int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, b
     if (rc) return rc;
     HIP_TRY(c, launch_fused<T>(a, st ? st : c->stream));
     return timed ? ev_end(c, ev, EV_FUSED, (long long)ncols * c->ny) : IBLB_OK;
+}
+
+template <typename T>
+int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, bool timed = true,
+                      hipStream_t st = nullptr) {
+    return launch_fused_at<T>(c, c->cur, col_begin, ncols, col_step, timed, st);
 }
 
 int free_boot(iblb_ctx* c) {
@@ -422,6 +461,114 @@ int overlapped_step(iblb_ctx* c) {
 // on the comm stream by an overlapped step).
 int join_comm(iblb_ctx* c) {
     if (c->comm_stream) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
+    return IBLB_OK;
+}
+
+// ---- two-thread batches of overlapped steps ---------------------------------------------------
+// Step s of a batch, like overlapped_step but with per-parity events:
+//   comm thread:   exchange(s) -> [int_issued >= s-1] wait ev_i[s-1] -> boundary(s) -> ev_b[s]
+//   caller thread: [bnd_issued >= s-1] wait ev_b[s-1] -> interior(s) -> ev_i[s]
+// A wait is issued only after the record it refers to (the counters), and an event is
+// recorded again (step s+2) only after the other thread has issued its wait on it.
+bool spin_until(const std::atomic<long long>& v, long long want, const std::atomic<int>& err) {
+    while (v.load(std::memory_order_acquire) < want) {
+        if (err.load(std::memory_order_acquire)) return false;
+        std::this_thread::yield();
+    }
+    return true;
+}
+
+template <typename T>
+int comm_batch(iblb_ctx* c, long long t0, long long n, int cur0) {
+    auto* ct = c->ct;
+    for (long long s = t0; s < t0 + n; ++s) {
+        const int cur = cur0 ^ (int)((s - t0) & 1);
+        int rc = exchange_rccl_raw(c, c->comm_stream);
+        if (rc) return rc;
+        if (!spin_until(ct->int_issued, s - 1, ct->err)) return IBLB_ERR_STATE;
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, ct->ev_i[(s - 1) & 1], 0));
+        if ((rc = launch_fused_at<T>(c, cur, 0, 2, c->ncol - 1, false, c->comm_stream))) return rc;
+        HIP_TRY(c, hipEventRecord(ct->ev_b[s & 1], c->comm_stream));
+        ct->bnd_issued.store(s, std::memory_order_release);
+    }
+    return IBLB_OK;
+}
+
+void comm_main(iblb_ctx* c) {
+    auto* ct = c->ct;
+    (void)hipSetDevice(c->device);
+    long long seen = 0;
+    for (;;) {
+        long long t0, n;
+        int cur0;
+        {
+            std::unique_lock<std::mutex> lk(ct->mu);
+            ct->cv.wait(lk, [&] { return ct->stop || ct->gen != seen; });
+            if (ct->stop) return;
+            seen = ct->gen;
+            t0 = ct->t0;
+            n = ct->n;
+            cur0 = ct->cur0;
+        }
+        const int rc = c->prec == IBLB_PREC_F64 ? comm_batch<double>(c, t0, n, cur0) : comm_batch<float>(c, t0, n, cur0);
+        if (rc) ct->err.store(rc, std::memory_order_release);
+        ct->bnd_issued.store(t0 + n, std::memory_order_release);  // batch over (done or failed)
+    }
+}
+
+bool batch_ready(const iblb_ctx* c) {
+    return c->ct && c->phase == PH_RUN && rccl_multi(c) && c->overlap && !c->prof && !c->cilia_on && !ib_active(c) &&
+           c->ncol >= 3;
+}
+
+template <typename T>
+int batch_steps(iblb_ctx* c, long long n) {
+    auto* ct = c->ct;
+    const long long t0 = c->t;
+    const int cur0 = c->cur;
+    int rc = join_comm(c);  // after the boundary columns of the current state
+    if (rc) return rc;
+    // "step t0-1" = everything issued so far; the comm stream starts after it
+    HIP_TRY(c, hipEventRecord(ct->ev_b[(t0 - 1) & 1], c->stream));
+    HIP_TRY(c, hipEventRecord(ct->ev_i[(t0 - 1) & 1], c->stream));
+    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, ct->ev_b[(t0 - 1) & 1], 0));
+    ct->err.store(0);
+    ct->bnd_issued.store(t0 - 1);
+    ct->int_issued.store(t0 - 1);
+    {
+        std::lock_guard<std::mutex> lk(ct->mu);
+        ct->t0 = t0;
+        ct->n = n;
+        ct->cur0 = cur0;
+        ct->gen++;
+    }
+    ct->cv.notify_all();
+    auto issue = [&](long long s) -> int {
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, ct->ev_b[(s - 1) & 1], 0));
+        int r = launch_fused_at<T>(c, cur0 ^ (int)((s - t0) & 1), 1, c->ncol - 2, 1, false, c->stream);
+        if (r) return r;
+        HIP_TRY(c, hipEventRecord(ct->ev_i[s & 1], c->stream));
+        return IBLB_OK;
+    };
+    for (long long s = t0; s < t0 + n; ++s) {
+        if (!spin_until(ct->bnd_issued, s - 1, ct->err)) break;
+        if ((rc = issue(s))) {
+            ct->err.store(rc, std::memory_order_release);
+            break;
+        }
+        ct->int_issued.store(s, std::memory_order_release);
+    }
+    // the comm thread has issued everything (or stopped) once bnd_issued passes the batch
+    while (ct->bnd_issued.load(std::memory_order_acquire) < t0 + n) std::this_thread::yield();
+    if (int e = ct->err.load()) return rc ? rc : e;
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, ct->ev_b[(t0 + n - 1) & 1], 0));
+    HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+    c->cur = cur0 ^ (int)(n & 1);
+    c->t = t0 + n;
+    c->halo_valid = false;
+    c->ib_state = IB_NONE;
     return IBLB_OK;
 }
 
@@ -692,6 +839,20 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
 void iblb_destroy(iblb_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->ct) {
+        {
+            std::lock_guard<std::mutex> lk(c->ct->mu);
+            c->ct->stop = true;
+        }
+        c->ct->cv.notify_all();
+        if (c->ct->thr.joinable()) c->ct->thr.join();
+        for (int p = 0; p < 2; ++p) {
+            if (c->ct->ev_b[p]) (void)hipEventDestroy(c->ct->ev_b[p]);
+            if (c->ct->ev_i[p]) (void)hipEventDestroy(c->ct->ev_i[p]);
+        }
+        delete c->ct;
+        c->ct = nullptr;
+    }
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->comm) ncclCommDestroy(c->comm);
@@ -868,8 +1029,15 @@ int iblb_step(iblb_ctx* c, int nsteps) {
     int rc = check_ready(c);
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
-    for (int s = 0; s < nsteps; ++s)
+    for (int s = 0; s < nsteps;) {
+        if (batch_ready(c)) {  // the rest as one two-thread batch
+            if ((rc = c->prec == IBLB_PREC_F64 ? batch_steps<double>(c, nsteps - s) : batch_steps<float>(c, nsteps - s)))
+                return rc;
+            break;
+        }
         if ((rc = step_one(c))) return rc;
+        ++s;
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return IBLB_OK;
 }
@@ -1206,6 +1374,14 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
+        if (c->overlap && env_long("IBLB_COMM_THREAD", 1) != 0 && !c->ct) {
+            c->ct = new iblb_ctx::CommThread();
+            for (int p = 0; p < 2; ++p) {
+                HIP_TRY(c, hipEventCreateWithFlags(&c->ct->ev_b[p], hipEventDisableTiming));
+                HIP_TRY(c, hipEventCreateWithFlags(&c->ct->ev_i[p], hipEventDisableTiming));
+            }
+            c->ct->thr = std::thread(comm_main, c);
+        }
     }
     c->halo_valid = false;
     int rc = pack_send(c);  // a restored state has no send buffers yet
