@@ -15,15 +15,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
-#include <atomic>
 #include <cmath>
-#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../../include/iblb.h"
@@ -113,25 +109,16 @@ struct iblb_ctx {
     bool self_ring = false;  // one rank that is its own neighbour over RCCL (IBLB_RCCL_SELF, rehearsal)
     std::vector<int> slab_begin, slab_count;  // every rank's columns (RCCL group)
     hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with the interior
-    hipEvent_t ev_bnd = nullptr;  // boundary columns + send buffers of the state written (either stream)
-    hipEvent_t ev_int = nullptr;  // compute-stream work of the last step done
+    hipEvent_t ev_bnd = nullptr;  // state (and its send buffers) written on the compute stream
     bool overlap = true;
-    // A second host thread issues the comm-stream half of a batch of overlapped steps (RCCL
-    // group, boundary launch), the caller's thread the interior launches (IBLB_COMM_THREAD=0:
-    // one thread issues both).  Host counters order the event records and waits.
-    struct CommThread {
-        std::thread thr;
-        std::mutex mu;
-        std::condition_variable cv;
-        bool stop = false;
-        long long t0 = 0, n = 0, gen = 0;   // current batch: steps [t0, t0+n), generation
-        int cur0 = 0;
-        std::atomic<long long> bnd_issued{0}, int_issued{0};  // last step whose record is issued
-        std::atomic<int> err{0};
-        hipEvent_t ev_b[2] = {nullptr, nullptr};  // boundary(s) done, by step parity
-        hipEvent_t ev_i[2] = {nullptr, nullptr};  // interior(s) done
-    };
-    CommThread* ct = nullptr;
+    // Pipelined halo: the collide launch runs the two boundary columns first and their last
+    // wave bumps *sig (signal memory); the comm stream waits for that value and exchanges the
+    // new boundary planes while the rest of the launch runs.  comm_ahead: an exchange of the
+    // current state's halo is in flight on the comm stream (ev_comm marks its end).
+    uint64_t* sig = nullptr;
+    uint64_t sig_target = 0;
+    bool comm_ahead = false;
+    hipEvent_t ev_comm = nullptr;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -278,20 +265,6 @@ int exchange_rccl(iblb_ctx* c, hipStream_t st, bool ib = false) {
     return ev_end(c, ev, EV_HALO, 0, st);
 }
 
-// the streaming halo exchange as the comm thread issues it (no profiling, no context state)
-int exchange_rccl_raw(iblb_ctx* c, hipStream_t st) {
-    const size_t n = (size_t)HALO_SLOTS * c->L.rows;
-    const ncclDataType_t dt = c->prec == IBLB_PREC_F64 ? ncclFloat64 : ncclFloat32;
-    const int lr = (c->rank + c->nranks - 1) % c->nranks, rr = (c->rank + 1) % c->nranks;
-    NCCL_TRY(c, ncclGroupStart());
-    NCCL_TRY(c, ncclSend(c->send_right, n, dt, rr, c->comm, st));
-    NCCL_TRY(c, ncclSend(c->send_left, n, dt, lr, c->comm, st));
-    NCCL_TRY(c, ncclRecv(c->recv_left, n, dt, lr, c->comm, st));
-    NCCL_TRY(c, ncclRecv(c->recv_right, n, dt, rr, c->comm, st));
-    NCCL_TRY(c, ncclGroupEnd());
-    return IBLB_OK;
-}
-
 // local group: the neighbours' send buffers are complete (group_exchange packed them)
 int exchange_local(iblb_ctx* c, bool ib) {
     const size_t bytes = (size_t)(ib ? IB_HALO_SLOTS : HALO_SLOTS) * c->L.rows * c->esize;
@@ -318,8 +291,7 @@ int pack_send(iblb_ctx* c) {
     }
     if (rccl_multi(c)) {
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
-        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+        c->comm_ahead = false;
     }
     return IBLB_OK;
 }
@@ -388,7 +360,8 @@ int launch_boot_step(iblb_ctx* c) {
 }
 
 template <typename T>
-int launch_fused_at(iblb_ctx* c, int cur, int col_begin, int ncols, int col_step, bool timed, hipStream_t st) {
+int launch_fused_at(iblb_ctx* c, int cur, int col_begin, int ncols, int col_step, bool timed, hipStream_t st,
+                    bool signal = false) {
     FusedArgs<T> a;
     a.src = gptr<T>(c, cur);
     a.dst = gptr<T>(c, 1 - cur);
@@ -409,6 +382,8 @@ int launch_fused_at(iblb_ctx* c, int cur, int col_begin, int ncols, int col_step
     a.Q = c->d_Q;
     a.c = c->coef;
     a.variant = c->variant;
+    a.bnd_first = signal ? 1 : 0;
+    a.sig = signal ? c->sig : nullptr;
     size_t ev = 0;
     int rc = timed ? ev_begin(c, &ev) : IBLB_OK;
     if (rc) return rc;
@@ -437,138 +412,36 @@ void after_step(iblb_ctx* c) {
     c->ib_state = ib_active(c) ? IB_PENDING : IB_NONE;
 }
 
-// RCCL slab, no IB force owed.  Step t on two streams:
-//   comm:    exchange(t) [send buffers of g^{t-1}] -> wait int(t-1) -> boundary columns(t) -> ev_bnd
-//   compute: (waited for ev_bnd = boundary(t-1) in step_one) -> interior columns(t) -> ev_int
-// The interior needs nothing from the exchange, so the halo and the two boundary columns run
-// beside it (on the CUs the collide leaves free, IBLB_RESERVE_CUS): the step costs the interior
-// launch as long as exchange + boundary are shorter.  boundary(t) waits for interior(t-1): it
-// reads columns 1 and ncol-2 of g^{t-1} and overwrites columns of the buffer interior(t-1) read.
+// RCCL slab, no IB force owed.  One collide launch over the whole slab, the boundary columns
+// dispatched first; their waves signal (c->sig) when the new boundary planes are written and
+// the halo they read is consumed.  The comm stream waits for that value and exchanges the new
+// planes while the rest of the launch runs, so the next step finds its halo ready:
+//   compute: wait ev_comm(t) -> collide(t) [columns 0, ncol-1 first -> sig]
+//   comm:    wait sig >= boundary(t) -> exchange(t+1) -> ev_comm(t+1)
 template <typename T>
 int overlapped_step(iblb_ctx* c) {
-    int rc = exchange_rccl(c, c->comm_stream);
-    if (rc) return rc;
-    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_int, 0));
-    if ((rc = launch_fused_step<T>(c, 0, 2, c->ncol - 1, false, c->comm_stream))) return rc;
-    HIP_TRY(c, hipEventRecord(c->ev_bnd, c->comm_stream));
-    if ((rc = launch_fused_step<T>(c, 1, c->ncol - 2))) return rc;
-    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
-    after_step(c);
+    int rc;
+    if (!c->comm_ahead) {  // first step of a pipelined run: the halo of the current state now
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+        if ((rc = exchange_rccl(c, c->comm_stream))) return rc;
+        HIP_TRY(c, hipEventRecord(c->ev_comm, c->comm_stream));
+    }
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_comm, 0));
+    if ((rc = launch_fused_at<T>(c, c->cur, 0, c->ncol, 1, true, c->stream, true))) return rc;
+    c->sig_target += 2 * (uint64_t)c->nch;
+    HIP_TRY(c, hipStreamWaitValue64(c->comm_stream, c->sig, c->sig_target, hipStreamWaitValueGte,
+                                    ~(uint64_t)0));
+    after_step(c);  // the exchange below fetches the halo of the new state
+    if ((rc = exchange_rccl(c, c->comm_stream))) return rc;
+    HIP_TRY(c, hipEventRecord(c->ev_comm, c->comm_stream));
+    c->comm_ahead = true;
     return IBLB_OK;
 }
 
-// Compute stream after the boundary columns of the current state (they may have been written
-// on the comm stream by an overlapped step).
+// Compute stream after the halo exchange in flight (if any): the current state's halo is then
+// in the receive buffers for whatever comes next on the compute stream.
 int join_comm(iblb_ctx* c) {
-    if (c->comm_stream) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
-    return IBLB_OK;
-}
-
-// ---- two-thread batches of overlapped steps ---------------------------------------------------
-// Step s of a batch, like overlapped_step but with per-parity events:
-//   comm thread:   exchange(s) -> [int_issued >= s-1] wait ev_i[s-1] -> boundary(s) -> ev_b[s]
-//   caller thread: [bnd_issued >= s-1] wait ev_b[s-1] -> interior(s) -> ev_i[s]
-// A wait is issued only after the record it refers to (the counters), and an event is
-// recorded again (step s+2) only after the other thread has issued its wait on it.
-bool spin_until(const std::atomic<long long>& v, long long want, const std::atomic<int>& err) {
-    while (v.load(std::memory_order_acquire) < want) {
-        if (err.load(std::memory_order_acquire)) return false;
-        std::this_thread::yield();
-    }
-    return true;
-}
-
-template <typename T>
-int comm_batch(iblb_ctx* c, long long t0, long long n, int cur0) {
-    auto* ct = c->ct;
-    for (long long s = t0; s < t0 + n; ++s) {
-        const int cur = cur0 ^ (int)((s - t0) & 1);
-        int rc = exchange_rccl_raw(c, c->comm_stream);
-        if (rc) return rc;
-        if (!spin_until(ct->int_issued, s - 1, ct->err)) return IBLB_ERR_STATE;
-        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, ct->ev_i[(s - 1) & 1], 0));
-        if ((rc = launch_fused_at<T>(c, cur, 0, 2, c->ncol - 1, false, c->comm_stream))) return rc;
-        HIP_TRY(c, hipEventRecord(ct->ev_b[s & 1], c->comm_stream));
-        ct->bnd_issued.store(s, std::memory_order_release);
-    }
-    return IBLB_OK;
-}
-
-void comm_main(iblb_ctx* c) {
-    auto* ct = c->ct;
-    (void)hipSetDevice(c->device);
-    long long seen = 0;
-    for (;;) {
-        long long t0, n;
-        int cur0;
-        {
-            std::unique_lock<std::mutex> lk(ct->mu);
-            ct->cv.wait(lk, [&] { return ct->stop || ct->gen != seen; });
-            if (ct->stop) return;
-            seen = ct->gen;
-            t0 = ct->t0;
-            n = ct->n;
-            cur0 = ct->cur0;
-        }
-        const int rc = c->prec == IBLB_PREC_F64 ? comm_batch<double>(c, t0, n, cur0) : comm_batch<float>(c, t0, n, cur0);
-        if (rc) ct->err.store(rc, std::memory_order_release);
-        ct->bnd_issued.store(t0 + n, std::memory_order_release);  // batch over (done or failed)
-    }
-}
-
-bool batch_ready(const iblb_ctx* c) {
-    return c->ct && c->phase == PH_RUN && rccl_multi(c) && c->overlap && !c->prof && !c->cilia_on && !ib_active(c) &&
-           c->ncol >= 3;
-}
-
-template <typename T>
-int batch_steps(iblb_ctx* c, long long n) {
-    auto* ct = c->ct;
-    const long long t0 = c->t;
-    const int cur0 = c->cur;
-    int rc = join_comm(c);  // after the boundary columns of the current state
-    if (rc) return rc;
-    // "step t0-1" = everything issued so far; the comm stream starts after it
-    HIP_TRY(c, hipEventRecord(ct->ev_b[(t0 - 1) & 1], c->stream));
-    HIP_TRY(c, hipEventRecord(ct->ev_i[(t0 - 1) & 1], c->stream));
-    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, ct->ev_b[(t0 - 1) & 1], 0));
-    ct->err.store(0);
-    ct->bnd_issued.store(t0 - 1);
-    ct->int_issued.store(t0 - 1);
-    {
-        std::lock_guard<std::mutex> lk(ct->mu);
-        ct->t0 = t0;
-        ct->n = n;
-        ct->cur0 = cur0;
-        ct->gen++;
-    }
-    ct->cv.notify_all();
-    auto issue = [&](long long s) -> int {
-        HIP_TRY(c, hipStreamWaitEvent(c->stream, ct->ev_b[(s - 1) & 1], 0));
-        int r = launch_fused_at<T>(c, cur0 ^ (int)((s - t0) & 1), 1, c->ncol - 2, 1, false, c->stream);
-        if (r) return r;
-        HIP_TRY(c, hipEventRecord(ct->ev_i[s & 1], c->stream));
-        return IBLB_OK;
-    };
-    for (long long s = t0; s < t0 + n; ++s) {
-        if (!spin_until(ct->bnd_issued, s - 1, ct->err)) break;
-        if ((rc = issue(s))) {
-            ct->err.store(rc, std::memory_order_release);
-            break;
-        }
-        ct->int_issued.store(s, std::memory_order_release);
-    }
-    // the comm thread has issued everything (or stopped) once bnd_issued passes the batch
-    while (ct->bnd_issued.load(std::memory_order_acquire) < t0 + n) std::this_thread::yield();
-    if (int e = ct->err.load()) return rc ? rc : e;
-    HIP_TRY(c, hipStreamWaitEvent(c->stream, ct->ev_b[(t0 + n - 1) & 1], 0));
-    HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
-    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
-    c->cur = cur0 ^ (int)(n & 1);
-    c->t = t0 + n;
-    c->halo_valid = false;
-    c->ib_state = IB_NONE;
+    if (c->comm_stream && c->comm_ahead) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_comm, 0));
     return IBLB_OK;
 }
 
@@ -586,8 +459,18 @@ int advance(iblb_ctx* c) {
     }
     if (rccl_multi(c)) {  // the whole state was written on the compute stream
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
-        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+        c->comm_ahead = false;
+    }
+    if (const long dbg = env_long("IBLB_DEBUG_SYNC", 0)) {  // probe: cost of stream sync packets
+        static hipEvent_t e1 = nullptr, e2 = nullptr;
+        if (!e1) {
+            HIP_TRY(c, hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+            HIP_TRY(c, hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+            HIP_TRY(c, hipEventRecord(e2, c->stream));
+        }
+        if (dbg & 1) HIP_TRY(c, hipEventRecord(e1, c->stream));
+        if (dbg & 2) HIP_TRY(c, hipStreamWaitEvent(c->stream, e2, 0));
+        if (dbg & 4) HIP_TRY(c, hipStreamWaitEvent(c->stream, e1, 0));
     }
     after_step(c);
     return IBLB_OK;
@@ -623,8 +506,7 @@ int step_one(iblb_ctx* c) {
         }
         if ((rc = run_cilia(c))) return rc;
     }
-    if (c->phase == PH_RUN && rccl_multi(c) && c->overlap && !c->halo_valid && c->ib_state != IB_PENDING &&
-        c->ncol >= 3)
+    if (c->phase == PH_RUN && rccl_multi(c) && c->overlap && c->ib_state != IB_PENDING && c->ncol >= 3)
         return c->prec == IBLB_PREC_F64 ? overlapped_step<double>(c) : overlapped_step<float>(c);
     if (c->phase == PH_RUN) {
         if ((rc = ensure_halo(c))) return rc;
@@ -775,6 +657,17 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     if (hipSetDevice(c->device) != hipSuccess) return bail(fail(c, IBLB_ERR_HIP, "hipSetDevice failed"));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(c, IBLB_ERR_HIP, "hipStreamCreate failed"));
+    if (const long dm = env_long("IBLB_DEBUG_CUMASK", 0)) {  // probe: a CU-masked stream for a single slab
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) return bail(fail(c, IBLB_ERR_HIP, "props"));
+        std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0u);
+        for (int i = 0; i < prop.multiProcessorCount - (int)dm; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+        hipStream_t m = nullptr;
+        if (hipExtStreamCreateWithCUMask(&m, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+            return bail(fail(c, IBLB_ERR_HIP, "cumask"));
+        (void)hipStreamDestroy(c->stream);
+        c->stream = m;
+    }
 
     // slab layout: a column of a plane holds `rows` = ny rounded up to whole waves.
     //  interleaved (default, IBLB_LAYOUT=1): g[xc*col + k*plane + y], the 9 planes of a
@@ -839,26 +732,13 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
 void iblb_destroy(iblb_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->ct) {
-        {
-            std::lock_guard<std::mutex> lk(c->ct->mu);
-            c->ct->stop = true;
-        }
-        c->ct->cv.notify_all();
-        if (c->ct->thr.joinable()) c->ct->thr.join();
-        for (int p = 0; p < 2; ++p) {
-            if (c->ct->ev_b[p]) (void)hipEventDestroy(c->ct->ev_b[p]);
-            if (c->ct->ev_i[p]) (void)hipEventDestroy(c->ct->ev_i[p]);
-        }
-        delete c->ct;
-        c->ct = nullptr;
-    }
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
-    if (c->ev_int) (void)hipEventDestroy(c->ev_int);
+    if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
+    if (c->sig) (void)hipFree(c->sig);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->g_alloc) (void)hipFree(c->g_alloc);
     void* bufs[] = {c->cil_samples, c->cil_lasts, c->cil_bpoints,
@@ -876,6 +756,8 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
     if (!c) return IBLB_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));  // no exchange in flight
+    c->comm_ahead = false;
     const long N = (long)c->ncol * c->ny;
     const size_t nb = (size_t)N * sizeof(double);
     free_boot(c);
@@ -1029,15 +911,8 @@ int iblb_step(iblb_ctx* c, int nsteps) {
     int rc = check_ready(c);
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
-    for (int s = 0; s < nsteps;) {
-        if (batch_ready(c)) {  // the rest as one two-thread batch
-            if ((rc = c->prec == IBLB_PREC_F64 ? batch_steps<double>(c, nsteps - s) : batch_steps<float>(c, nsteps - s)))
-                return rc;
-            break;
-        }
+    for (int s = 0; s < nsteps; ++s)
         if ((rc = step_one(c))) return rc;
-        ++s;
-    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return IBLB_OK;
 }
@@ -1370,17 +1245,13 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         const int prio = env_long("IBLB_COMM_PRIORITY", 1) != 0 ? prio_hi : prio_lo;
         HIP_TRY(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_int, hipEventDisableTiming));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
-        if (c->overlap && env_long("IBLB_COMM_THREAD", 1) != 0 && !c->ct) {
-            c->ct = new iblb_ctx::CommThread();
-            for (int p = 0; p < 2; ++p) {
-                HIP_TRY(c, hipEventCreateWithFlags(&c->ct->ev_b[p], hipEventDisableTiming));
-                HIP_TRY(c, hipEventCreateWithFlags(&c->ct->ev_i[p], hipEventDisableTiming));
-            }
-            c->ct->thr = std::thread(comm_main, c);
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
+        if (!c->sig) {
+            HIP_TRY(c, hipExtMallocWithFlags((void**)&c->sig, sizeof(uint64_t), hipMallocSignalMemory));
+            HIP_TRY(c, hipMemset(c->sig, 0, sizeof(uint64_t)));
+            c->sig_target = 0;
         }
     }
     c->halo_valid = false;
@@ -1530,6 +1401,8 @@ int iblb_load_checkpoint(iblb_ctx* c, const char* path) {
     if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: restore the slabs before linking");
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));  // no exchange in flight
+    c->comm_ahead = false;
     File fl;
     fl.f = std::fopen(path, "rb");
     if (!fl.f) return fail(c, IBLB_ERR_ARG, std::string("cannot open ") + path);

@@ -15,7 +15,7 @@ for nx in 4096 1024 512; do
   row "plain $nx" "$OUT/b_${nx}.json"
 done
 for nx in 1024 512; do
-  for cfg in "IBLB_RESERVE_CUS=8" "IBLB_RESERVE_CUS=4" "IBLB_RESERVE_CUS=0" "IBLB_OVERLAP=0"; do
+  for cfg in "IBLB_RESERVE_CUS=8" "IBLB_RESERVE_CUS=4" "IBLB_RESERVE_CUS=16" "IBLB_RESERVE_CUS=0" "IBLB_OVERLAP=0"; do
     tag=$(echo "$cfg" | tr '= ' '_-')
     env $cfg timeout -k 10 200 python bench.py --nx $nx --ny 4096 --steps 400 --warmup 40 --no-cpu-baseline \
       --no-profile-events --rccl-self > "$OUT/s_${nx}_${tag}.json" 2> "$OUT/s_${nx}_${tag}.err" \
@@ -23,7 +23,7 @@ for nx in 1024 512; do
     row "self-ring $nx $cfg" "$OUT/s_${nx}_${tag}.json"
   done
 done
-IBLB_RESERVE_CUS=8 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof512s" -o trace \
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof512s" -o trace \
   -- python bench.py --nx 512 --ny 4096 --steps 200 --warmup 20 --no-cpu-baseline --no-profile-events --rccl-self \
   > /dev/null 2> "$OUT/prof512s.err" || { tail -20 "$OUT/prof512s.err"; exit 1; }
 echo "== done"

@@ -430,14 +430,14 @@ def test_interleaved_layout_identical(gpu, monkeypatch, precision):
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-@pytest.mark.parametrize("comm_thread", [1, 0])
-def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, comm_thread):
-    """Bulk stepping of an RCCL group: with IBLB_COMM_THREAD=1 a second host thread issues the
-    comm-stream half (RCCL group, boundary columns) of the batch.  Real RCCL (self ring); must
-    equal the plain single slab bit for bit, eager steps before and after included."""
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap):
+    """Bulk stepping of an RCCL group: the pipelined schedule (boundary columns first, the next
+    halo exchange started from an in-kernel signal while the launch runs) over real RCCL (self
+    ring), readers interleaved; must equal the plain single slab bit for bit."""
     from cuda_iblb_11_amd import workloads as W
     monkeypatch.setenv("IBLB_RCCL_SELF", "1")
-    monkeypatch.setenv("IBLB_COMM_THREAD", str(comm_thread))
+    monkeypatch.setenv("IBLB_OVERLAP", str(overlap))
     nx, ny = 96, 200
     rho, u = W.perturbed_state(nx, ny, 8)
     ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 2e-7))
