@@ -109,16 +109,9 @@ struct iblb_ctx {
     bool self_ring = false;  // one rank that is its own neighbour over RCCL (IBLB_RCCL_SELF, rehearsal)
     std::vector<int> slab_begin, slab_count;  // every rank's columns (RCCL group)
     hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with the interior
-    hipEvent_t ev_bnd = nullptr;  // state (and its send buffers) written on the compute stream
+    hipEvent_t ev_bnd = nullptr;  // boundary columns + send buffers of the state written (either stream)
+    hipEvent_t ev_int = nullptr;  // compute-stream work of the last step done
     bool overlap = true;
-    // Pipelined halo: the collide launch runs the two boundary columns first and their last
-    // wave bumps *sig (signal memory); the comm stream waits for that value and exchanges the
-    // new boundary planes while the rest of the launch runs.  comm_ahead: an exchange of the
-    // current state's halo is in flight on the comm stream (ev_comm marks its end).
-    uint64_t* sig = nullptr;
-    uint64_t sig_target = 0;
-    bool comm_ahead = false;
-    hipEvent_t ev_comm = nullptr;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -291,7 +284,8 @@ int pack_send(iblb_ctx* c) {
     }
     if (rccl_multi(c)) {
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-        c->comm_ahead = false;
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     return IBLB_OK;
 }
@@ -360,13 +354,13 @@ int launch_boot_step(iblb_ctx* c) {
 }
 
 template <typename T>
-int launch_fused_at(iblb_ctx* c, int cur, int col_begin, int ncols, int col_step, bool timed, hipStream_t st,
-                    bool signal = false) {
+int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, bool timed = true,
+                      hipStream_t st = nullptr) {
     FusedArgs<T> a;
-    a.src = gptr<T>(c, cur);
-    a.dst = gptr<T>(c, 1 - cur);
+    a.src = gptr<T>(c, c->cur);
+    a.dst = gptr<T>(c, 1 - c->cur);
     a.L = c->L;
-    a.H = halo_of<T>(c, cur);
+    a.H = halo_of<T>(c, c->cur);
     send_ptrs<T>(c, a.send_left, a.send_right);
     a.col_begin = col_begin;
     a.col_step = col_step;
@@ -382,19 +376,11 @@ int launch_fused_at(iblb_ctx* c, int cur, int col_begin, int ncols, int col_step
     a.Q = c->d_Q;
     a.c = c->coef;
     a.variant = c->variant;
-    a.bnd_first = signal ? 1 : 0;
-    a.sig = signal ? c->sig : nullptr;
     size_t ev = 0;
     int rc = timed ? ev_begin(c, &ev) : IBLB_OK;
     if (rc) return rc;
     HIP_TRY(c, launch_fused<T>(a, st ? st : c->stream));
     return timed ? ev_end(c, ev, EV_FUSED, (long long)ncols * c->ny) : IBLB_OK;
-}
-
-template <typename T>
-int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, bool timed = true,
-                      hipStream_t st = nullptr) {
-    return launch_fused_at<T>(c, c->cur, col_begin, ncols, col_step, timed, st);
 }
 
 int free_boot(iblb_ctx* c) {
@@ -412,36 +398,30 @@ void after_step(iblb_ctx* c) {
     c->ib_state = ib_active(c) ? IB_PENDING : IB_NONE;
 }
 
-// RCCL slab, no IB force owed.  One collide launch over the whole slab, the boundary columns
-// dispatched first; their waves signal (c->sig) when the new boundary planes are written and
-// the halo they read is consumed.  The comm stream waits for that value and exchanges the new
-// planes while the rest of the launch runs, so the next step finds its halo ready:
-//   compute: wait ev_comm(t) -> collide(t) [columns 0, ncol-1 first -> sig]
-//   comm:    wait sig >= boundary(t) -> exchange(t+1) -> ev_comm(t+1)
+// RCCL slab, no IB force owed.  Step t on two streams:
+//   comm:    exchange(t) [send buffers of g^{t-1}] -> wait int(t-1) -> boundary columns(t) -> ev_bnd
+//   compute: (waited for ev_bnd = boundary(t-1) in step_one) -> interior columns(t) -> ev_int
+// The interior needs nothing from the exchange, so the halo and the two boundary columns run
+// beside it (on the CUs the collide leaves free, IBLB_RESERVE_CUS): the step costs the interior
+// launch as long as exchange + boundary are shorter.  boundary(t) waits for interior(t-1): it
+// reads columns 1 and ncol-2 of g^{t-1} and overwrites columns of the buffer interior(t-1) read.
 template <typename T>
 int overlapped_step(iblb_ctx* c) {
-    int rc;
-    if (!c->comm_ahead) {  // first step of a pipelined run: the halo of the current state now
-        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
-        if ((rc = exchange_rccl(c, c->comm_stream))) return rc;
-        HIP_TRY(c, hipEventRecord(c->ev_comm, c->comm_stream));
-    }
-    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_comm, 0));
-    if ((rc = launch_fused_at<T>(c, c->cur, 0, c->ncol, 1, true, c->stream, true))) return rc;
-    c->sig_target += 2 * (uint64_t)c->nch;
-    HIP_TRY(c, hipStreamWaitValue64(c->comm_stream, c->sig, c->sig_target, hipStreamWaitValueGte,
-                                    ~(uint64_t)0));
-    after_step(c);  // the exchange below fetches the halo of the new state
-    if ((rc = exchange_rccl(c, c->comm_stream))) return rc;
-    HIP_TRY(c, hipEventRecord(c->ev_comm, c->comm_stream));
-    c->comm_ahead = true;
+    int rc = exchange_rccl(c, c->comm_stream);
+    if (rc) return rc;
+    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_int, 0));
+    if ((rc = launch_fused_step<T>(c, 0, 2, c->ncol - 1, false, c->comm_stream))) return rc;
+    HIP_TRY(c, hipEventRecord(c->ev_bnd, c->comm_stream));
+    if ((rc = launch_fused_step<T>(c, 1, c->ncol - 2))) return rc;
+    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+    after_step(c);
     return IBLB_OK;
 }
 
-// Compute stream after the halo exchange in flight (if any): the current state's halo is then
-// in the receive buffers for whatever comes next on the compute stream.
+// Compute stream after the boundary columns of the current state (they may have been written
+// on the comm stream by an overlapped step).
 int join_comm(iblb_ctx* c) {
-    if (c->comm_stream && c->comm_ahead) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_comm, 0));
+    if (c->comm_stream) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
     return IBLB_OK;
 }
 
@@ -459,18 +439,8 @@ int advance(iblb_ctx* c) {
     }
     if (rccl_multi(c)) {  // the whole state was written on the compute stream
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-        c->comm_ahead = false;
-    }
-    if (const long dbg = env_long("IBLB_DEBUG_SYNC", 0)) {  // probe: cost of stream sync packets
-        static hipEvent_t e1 = nullptr, e2 = nullptr;
-        if (!e1) {
-            HIP_TRY(c, hipEventCreateWithFlags(&e1, hipEventDisableTiming));
-            HIP_TRY(c, hipEventCreateWithFlags(&e2, hipEventDisableTiming));
-            HIP_TRY(c, hipEventRecord(e2, c->stream));
-        }
-        if (dbg & 1) HIP_TRY(c, hipEventRecord(e1, c->stream));
-        if (dbg & 2) HIP_TRY(c, hipStreamWaitEvent(c->stream, e2, 0));
-        if (dbg & 4) HIP_TRY(c, hipStreamWaitEvent(c->stream, e1, 0));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     after_step(c);
     return IBLB_OK;
@@ -506,7 +476,8 @@ int step_one(iblb_ctx* c) {
         }
         if ((rc = run_cilia(c))) return rc;
     }
-    if (c->phase == PH_RUN && rccl_multi(c) && c->overlap && c->ib_state != IB_PENDING && c->ncol >= 3)
+    if (c->phase == PH_RUN && rccl_multi(c) && c->overlap && !c->halo_valid && c->ib_state != IB_PENDING &&
+        c->ncol >= 3)
         return c->prec == IBLB_PREC_F64 ? overlapped_step<double>(c) : overlapped_step<float>(c);
     if (c->phase == PH_RUN) {
         if ((rc = ensure_halo(c))) return rc;
@@ -657,17 +628,6 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     if (hipSetDevice(c->device) != hipSuccess) return bail(fail(c, IBLB_ERR_HIP, "hipSetDevice failed"));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(c, IBLB_ERR_HIP, "hipStreamCreate failed"));
-    if (const long dm = env_long("IBLB_DEBUG_CUMASK", 0)) {  // probe: a CU-masked stream for a single slab
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) return bail(fail(c, IBLB_ERR_HIP, "props"));
-        std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0u);
-        for (int i = 0; i < prop.multiProcessorCount - (int)dm; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
-        hipStream_t m = nullptr;
-        if (hipExtStreamCreateWithCUMask(&m, (uint32_t)mask.size(), mask.data()) != hipSuccess)
-            return bail(fail(c, IBLB_ERR_HIP, "cumask"));
-        (void)hipStreamDestroy(c->stream);
-        c->stream = m;
-    }
 
     // slab layout: a column of a plane holds `rows` = ny rounded up to whole waves.
     //  interleaved (default, IBLB_LAYOUT=1): g[xc*col + k*plane + y], the 9 planes of a
@@ -737,8 +697,7 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
-    if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
-    if (c->sig) (void)hipFree(c->sig);
+    if (c->ev_int) (void)hipEventDestroy(c->ev_int);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->g_alloc) (void)hipFree(c->g_alloc);
     void* bufs[] = {c->cil_samples, c->cil_lasts, c->cil_bpoints,
@@ -756,8 +715,6 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
     if (!c) return IBLB_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));  // no exchange in flight
-    c->comm_ahead = false;
     const long N = (long)c->ncol * c->ny;
     const size_t nb = (size_t)N * sizeof(double);
     free_boot(c);
@@ -1245,14 +1202,10 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         const int prio = env_long("IBLB_COMM_PRIORITY", 1) != 0 ? prio_hi : prio_lo;
         HIP_TRY(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_int, hipEventDisableTiming));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
-        if (!c->sig) {
-            HIP_TRY(c, hipExtMallocWithFlags((void**)&c->sig, sizeof(uint64_t), hipMallocSignalMemory));
-            HIP_TRY(c, hipMemset(c->sig, 0, sizeof(uint64_t)));
-            c->sig_target = 0;
-        }
     }
     c->halo_valid = false;
     int rc = pack_send(c);  // a restored state has no send buffers yet
@@ -1401,8 +1354,6 @@ int iblb_load_checkpoint(iblb_ctx* c, const char* path) {
     if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: restore the slabs before linking");
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));  // no exchange in flight
-    c->comm_ahead = false;
     File fl;
     fl.f = std::fopen(path, "rb");
     if (!fl.f) return fail(c, IBLB_ERR_ARG, std::string("cannot open ") + path);

@@ -33,8 +33,6 @@ struct FusedArgs {
     double* Q;
     Coef c;
     int variant;        // kernel variant (MODE bits of lbm_kernels.hip), 0 = default
-    int bnd_first;      // column order 0, ncol-1, 1, 2, ... (the boundary columns are dispatched first)
-    uint64_t* sig;      // if set: every wave of column 0 / ncol-1 adds 1 after its stores (system scope)
 };
 
 // Launch geometry of the collide-stream kernel: one wave per (column, 64*V-row chunk).

@@ -120,10 +120,9 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (gw >= a.ncols * a.nch) return;
+    const int xc = a.col_begin + (gw / a.nch) * a.col_step;
+    const int ch = gw - (gw / a.nch) * a.nch;
     const Layout L = a.L;
-    const int o = gw / a.nch;
-    const int xc = a.bnd_first ? (o == 0 ? 0 : (o == 1 ? L.ncol - 1 : o - 1)) : a.col_begin + o * a.col_step;
-    const int ch = gw - o * a.nch;
     const int cs = ch * (64 * V);
     const int y0 = cs + lane * V;
     const long cb = (long)xc * L.col;
@@ -223,10 +222,6 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
     if (do_flux) {
         q = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, q);
-    }
-    if (a.sig && (xc == 0 || xc == L.ncol - 1)) {  // boundary planes + halo reads done: tell the comm stream
-        __threadfence_system();
-        if (lane == 0) __hip_atomic_fetch_add(a.sig, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

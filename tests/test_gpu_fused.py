@@ -432,9 +432,9 @@ def test_interleaved_layout_identical(gpu, monkeypatch, precision):
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("overlap", [1, 0])
 def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap):
-    """Bulk stepping of an RCCL group: the pipelined schedule (boundary columns first, the next
-    halo exchange started from an in-kernel signal while the launch runs) over real RCCL (self
-    ring), readers interleaved; must equal the plain single slab bit for bit."""
+    """Bulk stepping of an RCCL group: the two-stream schedule (halo exchange and boundary
+    columns on the comm stream beside the interior launch) over real RCCL (self ring), readers
+    interleaved; must equal the plain single slab bit for bit."""
     from cuda_iblb_11_amd import workloads as W
     monkeypatch.setenv("IBLB_RCCL_SELF", "1")
     monkeypatch.setenv("IBLB_OVERLAP", str(overlap))
