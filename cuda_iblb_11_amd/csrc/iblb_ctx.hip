@@ -59,6 +59,10 @@ struct iblb_ctx {
     long fplane = 0;
     int device = 0;
     int variant = 0;  // collide-stream kernel variant (IBLB_FUSED_VARIANT, tuning only)
+    // two iterations per launch (lbm_sweep.hip) where no IB force is owed in between:
+    // IBLB_SWEEP (on), IBLB_SWEEP_W columns per wave, IBLB_SWEEP_VS cells per lane, variant
+    bool sweep_on = true;
+    int sweep_w = 16, sweep_vs = 2, sweep_variant = 1;
     hipStream_t stream = nullptr;
     Coef coef{};
     // populations: two buffers in one allocation (deterministic relative placement of the
@@ -116,8 +120,8 @@ struct iblb_ctx {
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
-    double fused_ms = 0., ib_ms = 0., halo_ms = 0.;
-    long long fused_launches = 0, fused_cells = 0;
+    double fused_ms = 0., ib_ms = 0., halo_ms = 0., sweep_ms = 0.;
+    long long fused_launches = 0, fused_cells = 0, sweep_launches = 0, sweep_cells = 0;
     struct EvRec { int kind; size_t idx; long long cells; };
     std::vector<EvRec> ev_kind;
     std::string err;
@@ -185,10 +189,11 @@ void send_ptrs(iblb_ctx* c, T* sl[3], T* sr[3]) {
 }
 
 // ---- profiling --------------------------------------------------------------------------
-enum EvKind { EV_FUSED = 0, EV_IB = 1, EV_HALO = 2 };
+enum EvKind { EV_FUSED = 0, EV_IB = 1, EV_HALO = 2, EV_SWEEP = 3 };
 
 void ev_account(iblb_ctx* c, const iblb_ctx::EvRec& r, float ms) {
     if (r.kind == EV_FUSED) { c->fused_ms += ms; c->fused_launches++; c->fused_cells += r.cells; }
+    else if (r.kind == EV_SWEEP) { c->sweep_ms += ms; c->sweep_launches++; c->sweep_cells += r.cells; }
     else if (r.kind == EV_IB) c->ib_ms += ms;
     else c->halo_ms += ms;
 }
@@ -425,6 +430,40 @@ int join_comm(iblb_ctx* c) {
     return IBLB_OK;
 }
 
+// ---- two iterations per launch ---------------------------------------------------------------
+// A lone slab with no IB force owed before or between the two iterations (no IB points, no cilia).
+bool sweep_ready(const iblb_ctx* c) {
+    return c->sweep_on && c->phase == PH_RUN && single_slab(c) && !c->cilia_on && !ib_active(c) &&
+           c->ib_state == IB_NONE && c->ncol >= 2;
+}
+
+template <typename T>
+int sweep_step(iblb_ctx* c) {
+    Sweep2Args<T> a{};
+    a.src = gptr<T>(c, c->cur);
+    a.dst = gptr<T>(c, 1 - c->cur);
+    a.L = c->L;
+    a.col_begin = 0;
+    a.ncols = c->ncol;
+    a.W = c->sweep_w;
+    a.vs = c->sweep_vs;
+    a.variant = c->sweep_variant;
+    const int fc = c->cfg.flux_column - c->x_begin;
+    a.flux_col = (fc >= 0 && fc < c->ncol) ? fc : -1;
+    a.flux_norm = c->cfg.flux_norm;
+    a.Q = c->d_Q;
+    a.c = c->coef;
+    size_t ev = 0;
+    int rc = ev_begin(c, &ev);
+    if (rc) return rc;
+    HIP_TRY(c, launch_sweep2<T>(a, c->stream));
+    if ((rc = ev_end(c, ev, EV_SWEEP, (long long)c->ncol * c->ny))) return rc;
+    c->cur = 1 - c->cur;
+    c->t += 2;
+    c->halo_valid = false;
+    return IBLB_OK;
+}
+
 // One reference iteration for a context whose halo (if any) and force^t are in place.
 int advance(iblb_ctx* c) {
     int rc;
@@ -611,6 +650,12 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     // the interleaved layout: f64 = DPP row shift + nontemporal stores (5), f32 = nontemporal
     // loads and stores (3; 0.193 ms vs 0.218 ms planar variant 2, profiles/r01e_tune_f32.log)
     c->variant = (int)env_long("IBLB_FUSED_VARIANT", c->prec == IBLB_PREC_F64 ? 5 : 3);
+    c->sweep_on = env_long("IBLB_SWEEP", 1) != 0;
+    // measured on MI355X at 4096^2 (profiles/r01n_tune_*.log): f64 2 cells per lane, 16 columns
+    // per wave, nontemporal stores (0.254 ms/iteration vs 0.405 one-step); f32 4 cells, 32 columns
+    c->sweep_w = (int)env_long("IBLB_SWEEP_W", c->prec == IBLB_PREC_F64 ? 16 : 32);
+    c->sweep_vs = (int)env_long("IBLB_SWEEP_VS", c->prec == IBLB_PREC_F64 ? 2 : 4);
+    c->sweep_variant = (int)env_long("IBLB_SWEEP_VARIANT", 1);
     if (c->cfg.flux_column < 0) c->cfg.flux_column = c->nx - 5;
 
     const double tau = cfg->tau, tau2 = cfg->tau2, cs = 0.57735;
@@ -868,8 +913,15 @@ int iblb_step(iblb_ctx* c, int nsteps) {
     int rc = check_ready(c);
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
-    for (int s = 0; s < nsteps; ++s)
+    for (int s = 0; s < nsteps;) {
+        if (nsteps - s >= 2 && sweep_ready(c)) {
+            if ((rc = c->prec == IBLB_PREC_F64 ? sweep_step<double>(c) : sweep_step<float>(c))) return rc;
+            s += 2;
+            continue;
+        }
         if ((rc = step_one(c))) return rc;
+        ++s;
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return IBLB_OK;
 }
@@ -1000,9 +1052,12 @@ int iblb_get_timing(iblb_ctx* c, iblb_timing* t, int reset) {
     t->fused_bytes = 18.0 * (double)c->esize;
     t->cells = (long long)c->ncol * c->ny;
     t->fused_cells = c->fused_cells;
+    t->sweep_launches = c->sweep_launches;
+    t->sweep_ms = c->sweep_ms;
+    t->sweep_cells = c->sweep_cells;
     if (reset) {
-        c->fused_ms = c->ib_ms = c->halo_ms = 0.;
-        c->fused_launches = c->fused_cells = 0;
+        c->fused_ms = c->ib_ms = c->halo_ms = c->sweep_ms = 0.;
+        c->fused_launches = c->fused_cells = c->sweep_launches = c->sweep_cells = 0;
     }
     return IBLB_OK;
 }

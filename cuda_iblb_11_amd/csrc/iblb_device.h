@@ -174,6 +174,7 @@ struct Store<float> {
 // `rho` returns sum h (= rho - 1); the caller adds 1.
 template <typename R>
 __device__ __forceinline__ void moments(const R f[9], R& rho, R& mx, R& my) {
+#pragma clang fp contract(on)
     rho = f[0] + f[1] + f[2] + f[3] + f[4] + f[5] + f[6] + f[7] + f[8];
     mx = ((((f[1] - f[3]) + f[5]) - f[6]) - f[7]) + f[8];
     my = ((((f[2] - f[4]) + f[5]) + f[6]) - f[7]) - f[8];
@@ -190,6 +191,7 @@ __device__ __forceinline__ void moments(const R f[9], R& rho, R& mx, R& my) {
 // DEV: f holds deviations h = f - w and drho = rho - 1 (float storage).
 template <typename R, bool DEV>
 __device__ __forceinline__ void collide(R f[9], R rho, R drho, R ux, R uy, R Fx, R Fy, const Coef& c) {
+#pragma clang fp contract(on)  // fuse within a statement only: the same FMAs in every kernel
     const R op = (R)c.omega_p, om = (R)c.omega_m;
     const R a1 = (R)c.inv_2cs2, a2 = (R)c.inv_2cs4, ics2 = (R)c.inv_cs2, ics4 = (R)c.inv_cs4;
     const R usq = ux * ux + uy * uy;
@@ -223,6 +225,26 @@ __device__ __forceinline__ void collide(R f[9], R rho, R drho, R ux, R uy, R Fx,
         f[a] = f[a] + A + B;
         f[b] = f[b] + A - B;
     }
+}
+
+// One cell of a collide-stream step: f = the pulled populations f^t (deviations if DEV),
+// force = body force + IB force of this cell (double).  rho and u^t = (sum c f + force/2)/rho
+// (ImmersedBoundary.cu:249-255) from f, then collide in place; returns u_x (flux sample).
+// Contraction is per statement (fp contract(on)), not left to the backend, so the one-step and
+// the two-iteration kernels round every cell identically whatever code surrounds them.
+template <typename R, bool DEV>
+__device__ __forceinline__ R relax_cell(R f[9], double fx, double fy, const Coef& c) {
+#pragma clang fp contract(on)
+    R s, mx, my;
+    moments<R>(f, s, mx, my);
+    const R rho = DEV ? (R)1 + s : s;
+    const R Fx = (R)fx;
+    const R Fy = (R)fy;
+    const R inv = (R)1 / rho;
+    const R ux = (mx + (R)0.5 * Fx) * inv;
+    const R uy = (my + (R)0.5 * Fy) * inv;
+    collide<R, DEV>(f, rho, s, ux, uy, Fx, Fy, c);
+    return ux;
 }
 
 // ImmersedBoundary.cu:21-81, with the reference's float/double rounding points.

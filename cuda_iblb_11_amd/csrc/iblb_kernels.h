@@ -35,6 +35,43 @@ struct FusedArgs {
     int variant;        // kernel variant (MODE bits of lbm_kernels.hip), 0 = default
 };
 
+// Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.
+// 2-step halo of a slab (9 planes per side, slots of L.rows elements):
+//   from the left  neighbour: 0-2 col -1 {1,5,8}, 3-5 col -1 {0,2,4}, 6-8 col -2 {1,5,8}
+//   from the right neighbour: 0-2 col ncol {3,6,7}, 3-5 col ncol {0,2,4}, 6-8 col ncol+1 {3,6,7}
+// (slots 0-2 are the one-step halo, so a one-step launch can follow a two-step exchange).
+constexpr int SWEEP_HALO_SLOTS = 9;
+// slot of plane k of the d-th column beyond the slab edge (d = 0, 1) in the left / right 2-step
+// halo (-1: not carried)
+__host__ __device__ constexpr int sweep_slot(bool left, int d, int k) {
+    return (left ? cx(k) == 1 : cx(k) == -1) ? (d == 0 ? halo_slot(k) : 6 + halo_slot(k))
+                                             : (d == 0 && cx(k) == 0 ? 3 + (k == 0 ? 0 : (k == 2 ? 1 : 2)) : -1);
+}
+
+template <typename T>
+struct Sweep2Args {
+    const T* src;        // g^t
+    T* dst;              // g^{t+2} (the other buffer)
+    Layout L;
+    const T* recv_left;  // 2-step halos received from the neighbours; nullptr: single slab
+    const T* recv_right; //   (columns -2, -1, ncol, ncol+1 are the periodic images)
+    T* send_left;        // 2-step halo for the left neighbour (SWEEP_HALO_SLOTS slots), or nullptr
+    T* send_right;
+    int col_begin;       // output columns [col_begin, col_begin + ncols)
+    int ncols;
+    int W;               // output columns per sweep (wave)
+    int vs;              // cells per lane; rows, col and plane multiples of vs
+    int nch, nsweep;     // set by launch_sweep2
+    int variant;         // MODE bits (nontemporal loads / stores)
+    int flux_col;        // local column sampled for Q (both iterations), or -1
+    double flux_norm;
+    double* Q;
+    Coef c;
+};
+
+template <typename T>
+hipError_t launch_sweep2(Sweep2Args<T> a, hipStream_t s);
+
 // Launch geometry of the collide-stream kernel: one wave per (column, 64*V-row chunk).
 inline int chunks_per_column(int ny, int V) { return (ny + 64 * V - 1) / (64 * V); }
 

@@ -6,108 +6,9 @@
 // Reference data flow it replaces: equilibrium -> collision -> streaming -> macro ->
 // spread's u correction (LatticeBoltzmann.cu:30-411, ImmersedBoundary.cu:249-264),
 // ~824 B/LU there.
-#include "iblb_kernels.h"
+#include "lbm_vec.h"
 
 namespace iblb {
-
-namespace {
-
-template <typename T, int V>
-struct VT {
-    typedef T type __attribute__((ext_vector_type(V)));
-};
-
-// 16-byte load at a 16-byte aligned address.
-template <typename T, int V>
-__device__ __forceinline__ typename VT<T, V>::type lda(const T* p) {
-    return *reinterpret_cast<const typename VT<T, V>::type*>(p);
-}
-// 16-byte load at an element-aligned (misaligned by one element) address.
-template <typename T, int V>
-__device__ __forceinline__ typename VT<T, V>::type ldu(const T* p) {
-    typename VT<T, V>::type r;
-    __builtin_memcpy(&r, p, sizeof(r));
-    return r;
-}
-template <typename T, int V>
-__device__ __forceinline__ void sta(T* p, typename VT<T, V>::type v) {
-    *reinterpret_cast<typename VT<T, V>::type*>(p) = v;
-}
-
-// Compute type: double storage collides in double, float storage in float
-// (deviation form keeps rho ~ 1 out of the float mantissa).
-template <typename T>
-struct Calc { typedef double R; };
-template <>
-struct Calc<float> { typedef float R; };
-
-}  // namespace
-
-// Kernel variants (MODE bits), selected per context for A/B measurement:
-//   MODE_NT_STORE  populations written with nontemporal stores
-//   MODE_NT_LOAD   populations read with nontemporal loads (each element is read once)
-//   MODE_SHIFT     all planes loaded 16-B aligned; the +-1-row shift of the c_y != 0 planes
-//                  is done in registers (DPP wave_shr / wave_shl by one lane) with one scalar
-//                  load per wave for the element across the chunk edge, instead of
-//                  misaligned 16-B loads
-enum { MODE_NT_STORE = 1, MODE_NT_LOAD = 2, MODE_SHIFT = 4 };
-
-template <typename T, int V, int MODE>
-__device__ __forceinline__ typename VT<T, V>::type ld_plane(const T* p) {
-    typedef typename VT<T, V>::type vec;
-    if (MODE & MODE_NT_LOAD) return __builtin_nontemporal_load(reinterpret_cast<const vec*>(p));
-    return lda<T, V>(p);
-}
-template <typename T, int V, int MODE>
-__device__ __forceinline__ void st_plane(T* p, typename VT<T, V>::type v) {
-    typedef typename VT<T, V>::type vec;
-    if (MODE & MODE_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<vec*>(p));
-    else sta<T, V>(p, v);
-}
-
-// Move a 32/64-bit value one lane up (dir = +1: lane l receives lane l-1) or down
-// (dir = -1: lane l receives lane l+1) across the whole wave with DPP.
-template <int DIR>
-__device__ __forceinline__ int dpp_shift(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, DIR > 0 ? 0x138 : 0x130, 0xf, 0xf, false);
-}
-template <int DIR>
-__device__ __forceinline__ double lane_shift(double v) {
-    const int lo = dpp_shift<DIR>(__double2loint(v));
-    const int hi = dpp_shift<DIR>(__double2hiint(v));
-    return __hiloint2double(hi, lo);
-}
-template <int DIR>
-__device__ __forceinline__ float lane_shift(float v) {
-    return __int_as_float(dpp_shift<DIR>(__float_as_int(v)));
-}
-
-// Rows y0-1 .. y0+V-2 (DIR = +1, planes with c_y = +1) or y0+1 .. y0+V (DIR = -1) of plane
-// pointer p (column base), for a wave covering rows [cs, cs + 64V).
-template <typename T, int V, int MODE, int DIR>
-__device__ __forceinline__ typename VT<T, V>::type ld_shifted(const T* p, int y0, int cs, int lane) {
-    typedef typename VT<T, V>::type vec;
-    if (!(MODE & MODE_SHIFT)) return ldu<T, V>(p + y0 - DIR);
-    const vec a = ld_plane<T, V, MODE>(p + y0);
-    vec r;
-    if (DIR > 0) {
-        // element 0 = last element of the previous lane; lane 0: row cs-1 (scalar load)
-        T prev = lane_shift<+1>(a[V - 1]);
-        const T edge = p[cs - 1];
-        if (lane == 0) prev = edge;
-        r[0] = prev;
-#pragma unroll
-        for (int e = 1; e < V; ++e) r[e] = a[e - 1];
-    } else {
-        T next = lane_shift<-1>(a[0]);
-        const T edge = p[cs + 64 * V];
-        if (lane == 63) next = edge;
-#pragma unroll
-        for (int e = 0; e < V - 1; ++e) r[e] = a[e + 1];
-        r[V - 1] = next;
-    }
-    return r;
-}
 
 // One wave = one (column, chunk of 64*V rows); lane l owns rows y0 .. y0+V-1.
 // Column-uniform decisions (halo source, flux column, IB flag, send buffers) are
@@ -186,16 +87,8 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
 #pragma unroll
     for (int e = 0; e < V; ++e) {
         R f[9] = {(R)v0[e], (R)v1[e], (R)v2[e], (R)v3[e], (R)v4[e], (R)v5[e], (R)v6[e], (R)v7[e], (R)v8[e]};
-        R s, mx, my;
-        moments<R>(f, s, mx, my);
-        const R rho = DEV ? (R)1 + s : s;
-        const R Fx = (R)(a.c.gx + fxv[e]);
-        const R Fy = (R)(a.c.gy + fyv[e]);
-        const R inv = (R)1 / rho;
-        const R ux = (mx + (R)0.5 * Fx) * inv;
-        const R uy = (my + (R)0.5 * Fy) * inv;
+        const R ux = relax_cell<R, DEV>(f, a.c.gx + fxv[e], a.c.gy + fyv[e], a.c);
         if (do_flux && y0 + e < L.ny) q += (double)ux / a.flux_norm;
-        collide<R, DEV>(f, rho, s, ux, uy, Fx, Fy, a.c);
         v0[e] = (T)f[0]; v1[e] = (T)f[1]; v2[e] = (T)f[2]; v3[e] = (T)f[3]; v4[e] = (T)f[4];
         v5[e] = (T)f[5]; v6[e] = (T)f[6]; v7[e] = (T)f[7]; v8[e] = (T)f[8];
     }

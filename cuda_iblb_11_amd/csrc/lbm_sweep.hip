@@ -1,0 +1,301 @@
+// lbm_sweep.hip — two reference iterations per launch (temporal blocking along x).
+//
+// The one-step collide-stream kernel (lbm_kernels.hip) already moves the algorithmic minimum of
+// one iteration, 144 B/LU in f64, at ~96 % of the measured HBM copy rate.  Below that floor the
+// only lever is to touch the state less often: this kernel reads g^t once and writes g^{t+2}
+// once, keeping the intermediate post-collision state g^{t+1} in registers.
+//
+// One wave = one (sweep, chunk): a chunk of 64*VS rows (lane l owns rows y0 .. y0+VS-1) and a
+// sweep of W output columns [xa, xb).  The wave walks x = xa-1 .. xb:
+//   step 1  g1[x]   = collide(pull(g0)) for its rows, plus ONE extra cell per lane: lane 0 the row
+//                     below the chunk (cs-1), lane 63 the row above (cs+64*VS).  Those are the
+//                     only g1 values of other chunks that step 2 pulls (c_y = +-1 planes).
+//   step 2  g2[x-1] = collide(pull(g1)) from the register window g1[x-2] (planes 1,5,8),
+//                     g1[x-1] (0,2,4 and the wall cells), g1[x] (3,6,7); +-1-row pulls are DPP
+//                     lane shifts whose end lanes take the extra cells.
+// Per cell and iteration the arithmetic is the one of fused_kernel (same relax_cell, same
+// storage rounding), so the result is bit-identical to two one-step launches.  Cost: the g1
+// columns xa-1 and xb are recomputed by the neighbouring sweeps and each lane collides VS+1
+// cells in step 1 (the extra cell is live in 2 lanes of 64).
+//
+// Algorithmic HBM bytes per launch: one read + one write of the state = 144 B per cell (f64) for
+// TWO lattice updates, plus the (W+2)/W re-read of the sweep edges.
+//
+// Single slab: columns -2, -1, ncol, ncol+1 are the periodic images.  Slab of a group: they come
+// from the 2-step halo (9 planes per side, slots in iblb_device.h: SWEEP_HALO_SLOTS), and the
+// kernel writes the 9 planes its neighbours need into the send buffers.
+#include "lbm_vec.h"
+
+namespace iblb {
+
+namespace {
+
+// pointer to plane k of column x (x in [-2, ncol+1]); x is wave-uniform.  Computed, not looked
+// up: a table of halo pointers in the kernel arguments costs more SGPRs than a wave has.
+template <typename T>
+__device__ __forceinline__ const T* sweep_col(const Sweep2Args<T>& a, int x, int k) {
+    const Layout& L = a.L;
+    const int xw = x < 0 ? x + L.ncol : (x >= L.ncol ? x - L.ncol : x);  // single slab: periodic image
+    return a.src + (long)xw * L.col + (long)k * L.plane;
+}
+
+// rows y0 .. y0+VS-1 of plane pointer p shifted by one row: DIR = +1 -> rows y-1, DIR = -1 ->
+// rows y+1, built from the aligned values v of this lane's rows; the end lane takes `edge`
+template <typename T, int VS, int DIR>
+__device__ __forceinline__ void shift_rows(const T v[VS], T edge, int lane, T r[VS]) {
+    if (DIR > 0) {
+        T prev = lane_shift<+1>(v[VS - 1]);
+        if (lane == 0) prev = edge;
+        r[0] = prev;
+#pragma unroll
+        for (int e = 1; e < VS; ++e) r[e] = v[e - 1];
+    } else {
+        T next = lane_shift<-1>(v[0]);
+        if (lane == 63) next = edge;
+#pragma unroll
+        for (int e = 0; e < VS - 1; ++e) r[e] = v[e + 1];
+        r[VS - 1] = next;
+    }
+}
+
+// Row-vector access at a wave-uniform base + this lane's 32-bit byte offset: the compiler keeps
+// the base in SGPRs (global_load/store saddr form) and every access shares one offset VGPR.
+// readfirstlane makes the base an opaque SGPR value, so the compiler cannot re-associate the
+// lane offset into a per-lane 64-bit address (2 VGPRs per access).
+template <typename P>
+__device__ __forceinline__ P* sgpr_ptr(P* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (P*)(((uint64_t)hi << 32) | lo);
+}
+#define IBLB_GLOBAL __attribute__((address_space(1)))
+
+template <typename T, int VS, int MODE>
+__device__ __forceinline__ void ld_rows(const T* base, unsigned off, T v[VS]) {
+    typedef typename VT<T, VS>::type vec;
+    const IBLB_GLOBAL vec* p = (const IBLB_GLOBAL vec*)((const IBLB_GLOBAL char*)sgpr_ptr(base) + off);
+    const vec x = (MODE & MODE_NT_LOAD) ? __builtin_nontemporal_load(p) : *p;
+#pragma unroll
+    for (int e = 0; e < VS; ++e) v[e] = x[e];
+}
+
+template <typename T, int VS, int MODE>
+__device__ __forceinline__ void st_rows(T* base, unsigned off, const T v[VS]) {
+    typedef typename VT<T, VS>::type vec;
+    vec x;
+#pragma unroll
+    for (int e = 0; e < VS; ++e) x[e] = v[e];
+    IBLB_GLOBAL vec* p = (IBLB_GLOBAL vec*)((IBLB_GLOBAL char*)sgpr_ptr(base) + off);
+    if (MODE & MODE_NT_STORE) __builtin_nontemporal_store(x, p);
+    else *p = x;
+}
+
+// Raw g0 rows of one column step: the 9 source planes at this lane's rows, plus the same-cell
+// values the walls need from planes whose pull column is not x (7, 8 at y = 0; 5, 6 at y = Y-1)
+template <typename T, int VS>
+struct Raw {
+    T v[9][VS];
+    T e[9];  // wave-edge rows: row0-1 of the c_y = +1 planes, row0+64*VS of the c_y = -1 planes
+    T w[4];  // g0(x, 0, 7), g0(x, 0, 8), g0(x, Y-1, 5), g0(x, Y-1, 6) (wall lanes only)
+};
+
+// rows of the wave start at row0 = cs - VS (uniform); lane byte offset off
+template <typename T, int VS, int MODE>
+__device__ __forceinline__ void load_raw(const Sweep2Args<T>& a, int x, int row0, unsigned off, bool bot, bool top,
+                                         Raw<T, VS>& r) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const T* p = sweep_col<T>(a, x - cx(k), k) + row0;
+        ld_rows<T, VS, MODE>(p, off, r.v[k]);
+        // the ghost lanes' own pulls reach one row beyond the wave (uniform address)
+        if (cy(k) == 1) r.e[k] = p[-1];
+        if (cy(k) == -1) r.e[k] = p[64 * VS];
+    }
+    r.w[0] = r.w[1] = r.w[2] = r.w[3] = (T)0;
+    if (bot) {
+        r.w[0] = sweep_col<T>(a, x, 7)[0];
+        r.w[1] = sweep_col<T>(a, x, 8)[0];
+    }
+    if (top) {
+        r.w[2] = sweep_col<T>(a, x, 5)[a.L.ny - 1];
+        r.w[3] = sweep_col<T>(a, x, 6)[a.L.ny - 1];
+    }
+}
+
+// pull of the 9 populations of this lane's rows from one column triple of a post-collision
+// state held as aligned row vectors (pk[k]: plane k of column x - c_x(k)): planes with c_y = 0 as
+// they are, c_y = +1 from the row below (DPP shift up), c_y = -1 from the row above, the end
+// lanes taking edge[k] (the row beyond the wave; nullptr: garbage, see below); the walls
+// from the same cell of the middle column (planes 2, 4 of this lane's rows, 7 and 8 of row 0,
+// 5 and 6 of this lane's rows for the top row).  The end lanes' out-of-wave neighbours are garbage: those lanes are the
+// sweep's ghost rows.
+template <typename T, int VS>
+__device__ __forceinline__ void pull_window(const T (*pk[9])[VS], const T* edge, const T (&m2)[VS], const T (&m4)[VS],
+                                            T m7, T m8, const T (&m5)[VS], const T (&m6)[VS], int lane, int r0,
+                                            int et, T s[9][VS]) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        if (cy(k) == 0) {
+#pragma unroll
+            for (int e = 0; e < VS; ++e) s[k][e] = (*pk[k])[e];
+        } else if (cy(k) == 1) {
+            shift_rows<T, VS, +1>(*pk[k], edge ? edge[k] : (T)0, lane, s[k]);
+        } else {
+            shift_rows<T, VS, -1>(*pk[k], edge ? edge[k] : (T)0, lane, s[k]);
+        }
+    }
+    if (r0 == 0) {  // bounce-back on y = 0 (LatticeBoltzmann.cu:328-340)
+        s[2][0] = m4[0];
+        s[5][0] = m7;
+        s[6][0] = m8;
+    }
+    if (et >= 0 && et < VS) {  // same-cell mirror on y = Y-1 (LatticeBoltzmann.cu:341-353)
+#pragma unroll
+        for (int e = 0; e < VS; ++e)
+            if (e == et) { s[4][e] = m2[e]; s[8][e] = m5[e]; s[7][e] = m6[e]; }
+    }
+}
+
+}  // namespace
+
+// One wave = (sweep, chunk).  Lane l holds rows r0 = cs - VS + l*VS .. r0+VS-1: lanes 1..62 own
+// the chunk's 62*VS output rows [cs, cs + 62*VS), lanes 0 and 63 are ghost rows (the g1 values
+// of the rows just outside the chunk that step 2 pulls).  Ghost rows and rows >= ny compute
+// garbage that no owned row reads.
+template <typename T, int VS, int MODE>
+__global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
+    typedef typename Calc<T>::R R;
+    static_assert(sizeof(R) == sizeof(T), "the window keeps g1 in the storage type");
+    constexpr bool DEV = Store<T>::dev;
+    const int lane = threadIdx.x & 63;
+    const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (gw >= a.nsweep * a.nch) return;
+    const Layout L = a.L;
+    const int sw = gw / a.nch;
+    const int ch = gw - sw * a.nch;
+    const int xa = a.col_begin + sw * a.W;
+    const int xb = min(xa + a.W, a.col_begin + a.ncols);
+    const int cs = ch * (62 * VS);
+    const int row0 = cs - VS;  // first row of the wave (lane 0)
+    const int r0 = row0 + lane * VS;
+    const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
+    const int et = L.ny - 1 - r0;  // element of the top row, if in [0, VS)
+    const bool owner = lane >= 1 && lane <= 62 && r0 < L.ny;
+    const bool bot = r0 == 0;
+    const bool top = et >= 0 && et < VS;
+    const double gx = a.c.gx, gy = a.c.gy;
+
+    // g1 window: A = g1[x-2] (planes 1, 5, 8 used), B = g1[x-1], C = g1[x]
+    T A[9][VS], B[9][VS];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int e = 0; e < VS; ++e) { A[k][e] = 0; B[k][e] = 0; }
+    double q = 0.;
+
+    Raw<T, VS> nxt;
+    load_raw<T, VS, MODE>(a, xa - 1, row0, off, bot, top, nxt);
+    for (int x = xa - 1; x <= xb; ++x) {
+        const Raw<T, VS> cur = nxt;
+        load_raw<T, VS, MODE>(a, min(x + 1, xb), row0, off, bot, top, nxt);
+
+        // ---- step 1: g1[x] ----
+        T C[9][VS];
+        {
+            const T(*pk[9])[VS];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) pk[k] = &cur.v[k];
+            T s[9][VS];
+            T t5[VS], t6[VS];
+#pragma unroll
+            for (int e = 0; e < VS; ++e) { t5[e] = cur.w[2]; t6[e] = cur.w[3]; }
+            pull_window<T, VS>(pk, cur.e, cur.v[2], cur.v[4], cur.w[0], cur.w[1], t5, t6, lane, r0, et, s);
+            const bool flux1 = x == a.flux_col && x >= xa && x < xb;
+#pragma unroll
+            for (int e = 0; e < VS; ++e) {
+                R f[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
+                const R ux = relax_cell<R, DEV>(f, gx, gy, a.c);
+                if (flux1 && owner && r0 + e < L.ny) q += (double)ux / a.flux_norm;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) C[k][e] = (T)f[k];
+            }
+        }
+
+        // ---- step 2: g2[x-1] from the window ----
+        if (x > xa) {
+            const int xo = x - 1;
+            const T(*pk[9])[VS];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) pk[k] = cx(k) == 1 ? &A[k] : (cx(k) == -1 ? &C[k] : &B[k]);
+            T s[9][VS];
+            pull_window<T, VS>(pk, nullptr, B[2], B[4], B[7][0], B[8][0], B[5], B[6], lane, r0, et, s);
+            const bool flux2 = xo == a.flux_col;
+#pragma unroll
+            for (int e = 0; e < VS; ++e) {
+                R f[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
+                const R ux = relax_cell<R, DEV>(f, gx, gy, a.c);
+                if (flux2 && owner && r0 + e < L.ny) q += (double)ux / a.flux_norm;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) s[k][e] = (T)f[k];
+            }
+            if (owner) {
+                T* dst = a.dst + (long)xo * L.col + row0;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * L.plane, off, s[k]);
+            }
+        }
+
+        // ---- rotate the window ----
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+#pragma unroll
+            for (int e = 0; e < VS; ++e) { A[k][e] = B[k][e]; B[k][e] = C[k][e]; }
+    }
+    if (a.flux_col >= xa && a.flux_col < xb) {
+        q = wave_sum(q);
+        if (lane == 0) atomicAdd(a.Q, q);
+    }
+}
+
+template <typename T, int VS, int MODE>
+static hipError_t launch_sweep_mode(const Sweep2Args<T>& a, unsigned blocks, hipStream_t s) {
+    sweep2_kernel<T, VS, MODE><<<blocks, 256, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+template <typename T, int VS>
+static hipError_t launch_sweep_vs(const Sweep2Args<T>& a, unsigned blocks, hipStream_t s) {
+    switch (a.variant) {
+        case 1: return launch_sweep_mode<T, VS, 1>(a, blocks, s);
+        case 2: return launch_sweep_mode<T, VS, 2>(a, blocks, s);
+        case 3: return launch_sweep_mode<T, VS, 3>(a, blocks, s);
+        default: return launch_sweep_mode<T, VS, 0>(a, blocks, s);
+    }
+}
+
+template <typename T>
+hipError_t launch_sweep2(Sweep2Args<T> a, hipStream_t s) {
+    if (a.ncols <= 0) return hipSuccess;
+    // rows are read up to VS below 0 and nch*62*VS + VS - 1 (< rows + 62*VS + VS): inside the
+    // 512-element guards of the buffers (iblb_ctx.hip)
+    if (a.W <= 0 || a.L.ncol < 2 || a.vs <= 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 || a.L.col % a.vs != 0)
+        return hipErrorInvalidValue;
+    a.nch = (a.L.ny + 62 * a.vs - 1) / (62 * a.vs);
+    a.nsweep = (a.ncols + a.W - 1) / a.W;
+    const long waves = (long)a.nsweep * a.nch;
+    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    constexpr int V = vec_of<T>();
+    if (a.vs == V) return launch_sweep_vs<T, V>(a, blocks, s);
+    if (a.vs == V / 2) return launch_sweep_vs<T, V / 2>(a, blocks, s);
+    return hipErrorInvalidValue;
+}
+
+template hipError_t launch_sweep2<double>(Sweep2Args<double>, hipStream_t);
+template hipError_t launch_sweep2<float>(Sweep2Args<float>, hipStream_t);
+
+}  // namespace iblb

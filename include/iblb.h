@@ -135,6 +135,11 @@ typedef struct iblb_timing {
     double    fused_bytes;     /* algorithmic bytes per cell of the collide-stream kernel */
     long long cells;           /* cells owned by this context                            */
     long long fused_cells;     /* lattice updates done by the timed collide-stream launches */
+    /* two-iteration launches (temporal blocking, lbm_sweep.hip): each reads and writes the
+     * state once (fused_bytes per cell) and advances its cells by two iterations */
+    long long sweep_launches;  /* timed two-iteration launches                           */
+    double    sweep_ms;        /* their summed duration                                  */
+    long long sweep_cells;     /* cells they covered (lattice updates = 2 x sweep_cells) */
 } iblb_timing;
 
 /* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */

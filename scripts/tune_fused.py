@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""A/B the collide-stream kernel variants in ONE process, interleaved rounds
+"""A/B the collide-stream kernel variants (one-step fused_kernel and the two-iteration sweep,
+IBLB_SWEEP*) in ONE process, interleaved rounds
 (cdna_hip_programming.md §5.4 rule 24).  Each variant gets its own context (IBLB_FUSED_VARIANT
 and IBLB_PLANE_PAD are read at iblb_create); results must be bit-identical across variants.
 
@@ -49,7 +50,8 @@ def main():
         for grp in a.envs.split(";"):
             e = dict(kv.split("=") for kv in grp.split())
             sets.append((grp, e))
-    names = sorted({k for _, e in sets for k in e} | {"IBLB_FUSED_VARIANT", "IBLB_PLANE_PAD", "IBLB_BUF_GAP"})
+    names = sorted({k for _, e in sets for k in e} | {"IBLB_FUSED_VARIANT", "IBLB_PLANE_PAD", "IBLB_BUF_GAP",
+                                                     "IBLB_SWEEP", "IBLB_SWEEP_W", "IBLB_SWEEP_VS", "IBLB_SWEEP_VARIANT"})
     ctxs = []
     for key, e in sets:
         for name in names:
@@ -68,7 +70,8 @@ def main():
             lat.timing(reset=True)
             lat.step(a.steps)
             t = lat.timing(reset=True)
-            res[k].append(t["fused_ms"] / t["fused_launches"])
+            # time per iteration: one-step launches count once, two-iteration sweeps twice
+            res[k].append((t["fused_ms"] + t["sweep_ms"]) / (t["fused_launches"] + 2 * t["sweep_launches"]))
         print(f"round {r} done", flush=True)
     bpc = 18 * (8 if a.precision == "f64" else 4)
     cells = a.nx * a.ny
@@ -77,8 +80,9 @@ def main():
         ms = np.array(res[k])
         r_, u_ = lat.macro()
         same = bool(np.array_equal(r_, ref_rho) and np.array_equal(u_, ref_u))
-        row = {"config": k, "median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
-               "tbps_median": bpc * cells / (np.median(ms) * 1e-3) / 1e12, "bitwise_equal_to_first": same}
+        row = {"config": k, "median_ms_per_iter": float(np.median(ms)), "min_ms": float(ms.min()),
+               "mlups": cells / (np.median(ms) * 1e-3) / 1e6,
+               "tbps_equiv_one_step": bpc * cells / (np.median(ms) * 1e-3) / 1e12, "bitwise_equal_to_first": same}
         print(json.dumps(row), flush=True)
 
 

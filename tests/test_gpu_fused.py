@@ -454,3 +454,43 @@ def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap):
     assert ring.steps == ref.steps == 107
     assert abs(ring.flux - ref.flux) <= 1e-13 * abs(ref.flux)  # per-chunk atomics: order varies
     ring.close()
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch):
+    """The two-iteration sweep kernel (g1 kept in registers, ghost lanes for the chunk edges,
+    periodic columns) equals pairs of one-step launches bit for bit, for every cells-per-lane
+    width, sweep length and load/store variant, on shapes with ragged chunks (ny not a multiple of
+    62*VS), fewer columns than one sweep, one-row-above-a-chunk tops and several chunks; odd step
+    counts end with a one-step launch.  Flux: same terms, other summation order."""
+    from cuda_iblb_11_amd import workloads as W
+    vss = [1, 2] if precision == "f64" else [2, 4]
+    for nx, ny in [(37, 300), (5, 1100), (2, 63), (70, 125), (33, 249)]:
+        rho, u = W.perturbed_state(nx, ny, 6)
+        monkeypatch.setenv("IBLB_SWEEP", "0")
+        ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 3e-7))
+        ref.set_state(rho, u)
+        ref.step(32)
+        f_ref, q_ref = ref.populations(), ref.flux
+        ref.close()
+        monkeypatch.setenv("IBLB_SWEEP", "1")
+        for vs in vss:
+            for w in (1, 3, 32):
+                for var in (0, 1, 2, 3):
+                    monkeypatch.setenv("IBLB_SWEEP_VS", str(vs))
+                    monkeypatch.setenv("IBLB_SWEEP_W", str(w))
+                    monkeypatch.setenv("IBLB_SWEEP_VARIANT", str(var))
+                    lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 3e-7))
+                    lat.set_state(rho, u)
+                    lat.set_profiling(True)
+                    lat.step(32)  # boot step, 15 sweeps, one one-step launch
+                    tm = lat.timing()
+                    assert tm["sweep_launches"] == 15 and tm["fused_launches"] == 1, tm
+                    f = lat.populations()
+                    assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, float(np.max(np.abs(f - f_ref))))
+                    assert abs(lat.flux - q_ref) <= 1e-12 * abs(q_ref), (lat.flux, q_ref)
+                    lat.close()
+    for name in ("IBLB_SWEEP_VS", "IBLB_SWEEP_W", "IBLB_SWEEP_VARIANT"):
+        monkeypatch.delenv(name)
+    lat, sim = run_pair(gpu, oracle, 70, 125, 40, precision=precision)
+    check_fields(lat, sim, TIGHT if precision == "f64" else TOL32)
