@@ -103,6 +103,7 @@ struct iblb_ctx {
     int ib_state = IB_NONE;
     bool halo_valid = false;
     bool halo_ib = false;  // the received halo carries the IB slots (IB_HALO_SLOTS)
+    bool send_sweep = false;  // the send buffers hold the 2-step halo of the current state
     int halo_slots = HALO_SLOTS;  // slots per halo buffer (IB_HALO_SLOTS when IB-capable)
     // transport
     int transport = TR_NONE;
@@ -243,13 +244,15 @@ int pack_ib_any(iblb_ctx* c, hipStream_t st) {
     return c->prec == IBLB_PREC_F64 ? pack_ib<double>(c, st) : pack_ib<float>(c, st);
 }
 
-// ib: also carry the IB slots (the owed force is evaluated from this halo)
-int exchange_rccl(iblb_ctx* c, hipStream_t st, bool ib = false) {
+// ib: also carry the IB slots (the owed force is evaluated from this halo); sweep: the 2-step
+// halo (the send buffers hold it: written by the boundary sweep or packed)
+int exchange_rccl(iblb_ctx* c, hipStream_t st, bool ib = false, bool sweep = false) {
     size_t ev = 0;
     int rc;
     if (ib && (rc = pack_ib_any(c, st))) return rc;
+    if (ib) c->send_sweep = false;  // slots 3.. now carry the IB halo
     if ((rc = ev_begin(c, &ev, st))) return rc;
-    const size_t n = (size_t)(ib ? IB_HALO_SLOTS : HALO_SLOTS) * c->L.rows;
+    const size_t n = (size_t)(ib ? IB_HALO_SLOTS : (sweep ? SWEEP_HALO_SLOTS : HALO_SLOTS)) * c->L.rows;
     const ncclDataType_t dt = c->prec == IBLB_PREC_F64 ? ncclFloat64 : ncclFloat32;
     const int lr = (c->rank + c->nranks - 1) % c->nranks, rr = (c->rank + 1) % c->nranks;
     NCCL_TRY(c, ncclGroupStart());
@@ -287,6 +290,7 @@ int pack_send(iblb_ctx* c) {
         HIP_TRY(c, hipMemcpyAsync((char*)c->send_left + p * c->L.rows * c->esize, l, n, hipMemcpyDeviceToDevice,
                                   c->stream));
     }
+    c->send_sweep = false;
     if (rccl_multi(c)) {
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
@@ -397,6 +401,7 @@ int free_boot(iblb_ctx* c) {
 }
 
 void after_step(iblb_ctx* c) {
+    c->send_sweep = false;  // a one-step collide writes the one-step slots only
     c->cur = 1 - c->cur;
     c->t++;
     c->halo_valid = false;
@@ -431,21 +436,33 @@ int join_comm(iblb_ctx* c) {
 }
 
 // ---- two iterations per launch ---------------------------------------------------------------
-// A lone slab with no IB force owed before or between the two iterations (no IB points, no cilia).
+// No IB force owed before or between the two iterations (no IB points, no cilia).  A lone slab:
+// one launch.  A slab of an RCCL group (>= 4 columns): the 2-step halo exchange and the boundary
+// sweeps (columns 0, 1, ncol-2, ncol-1) on the comm stream beside the interior sweep, like
+// overlapped_step:
+//   comm:    exchange(t) -> wait int(t-2) -> boundary(t) [+ 2-step send halo of g^{t+2}] -> ev_bnd
+//   compute: (join_comm: boundary(t-2)) -> interior columns [2, ncol-2)(t) -> ev_int
 bool sweep_ready(const iblb_ctx* c) {
-    return c->sweep_on && c->phase == PH_RUN && single_slab(c) && !c->cilia_on && !ib_active(c) &&
-           c->ib_state == IB_NONE && c->ncol >= 2;
+    if (!c->sweep_on || c->phase != PH_RUN || c->cilia_on || ib_active(c) || c->ib_state != IB_NONE) return false;
+    if (single_slab(c)) return c->ncol >= 2;
+    return rccl_multi(c) && c->ncol >= 4;
 }
 
 template <typename T>
-int sweep_step(iblb_ctx* c) {
+Sweep2Args<T> sweep_args(iblb_ctx* c, int col_begin, int col_step, int col_end, int nsweep, int W) {
     Sweep2Args<T> a{};
     a.src = gptr<T>(c, c->cur);
     a.dst = gptr<T>(c, 1 - c->cur);
     a.L = c->L;
-    a.col_begin = 0;
-    a.ncols = c->ncol;
-    a.W = c->sweep_w;
+    a.recv_left = (const T*)c->recv_left;
+    a.recv_right = (const T*)c->recv_right;
+    a.send_left = (T*)c->send_left;
+    a.send_right = (T*)c->send_right;
+    a.col_begin = col_begin;
+    a.col_step = col_step;
+    a.col_end = col_end;
+    a.nsweep = nsweep;
+    a.W = W;
     a.vs = c->sweep_vs;
     a.variant = c->sweep_variant;
     const int fc = c->cfg.flux_column - c->x_begin;
@@ -453,14 +470,63 @@ int sweep_step(iblb_ctx* c) {
     a.flux_norm = c->cfg.flux_norm;
     a.Q = c->d_Q;
     a.c = c->coef;
+    return a;
+}
+
+template <typename T>
+int sweep_launch(iblb_ctx* c, const Sweep2Args<T>& a, bool slab, hipStream_t st, bool timed, long long cells) {
     size_t ev = 0;
-    int rc = ev_begin(c, &ev);
+    int rc = timed ? ev_begin(c, &ev, st) : IBLB_OK;
     if (rc) return rc;
-    HIP_TRY(c, launch_sweep2<T>(a, c->stream));
-    if ((rc = ev_end(c, ev, EV_SWEEP, (long long)c->ncol * c->ny))) return rc;
+    HIP_TRY(c, launch_sweep2<T>(a, slab, st));
+    return timed ? ev_end(c, ev, EV_SWEEP, cells, st) : IBLB_OK;
+}
+
+void after_sweep(iblb_ctx* c) {
     c->cur = 1 - c->cur;
     c->t += 2;
     c->halo_valid = false;
+}
+
+template <typename T>
+int sweep_step(iblb_ctx* c) {
+    const int W = std::max(1, c->sweep_w);
+    if (single_slab(c)) {
+        int rc = sweep_launch<T>(c, sweep_args<T>(c, 0, W, c->ncol, (c->ncol + W - 1) / W, W), false, c->stream, true,
+                                 (long long)c->ncol * c->ny);
+        if (rc) return rc;
+        after_sweep(c);
+        return IBLB_OK;
+    }
+    int rc = join_comm(c);  // boundary columns of the current state (comm stream)
+    if (rc) return rc;
+    if (!c->send_sweep) {  // the send buffers hold the one-step (or IB) halo: pack the 2-step one
+        HIP_TRY(c, launch_pack_sweep_halo<T>(gptr<T>(c, c->cur), c->L, (T*)c->send_left, (T*)c->send_right,
+                                             c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+    }
+    const bool ov = c->overlap;
+    hipStream_t bs = ov ? c->comm_stream : c->stream;
+    if (!ov) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
+    if ((rc = exchange_rccl(c, bs, false, true))) return rc;
+    if (ov) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
+    // boundary sweeps: [0, 2) and [ncol-2, ncol)
+    if ((rc = sweep_launch<T>(c, sweep_args<T>(c, 0, c->ncol - 2, c->ncol, 2, 2), true, bs, false, 0))) return rc;
+    if (ov) HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
+    const int ni = c->ncol - 4;  // interior [2, ncol-2): needs nothing from the halo
+    if (ni > 0 && (rc = sweep_launch<T>(c, sweep_args<T>(c, 2, W, c->ncol - 2, (ni + W - 1) / W, W), false, c->stream,
+                                        true, (long long)ni * c->ny)))
+        return rc;
+    if (ov) HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+    else {
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+    }
+    after_sweep(c);
+    c->send_sweep = true;
     return IBLB_OK;
 }
 
@@ -707,9 +773,10 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
         c->g[0] = c->g_alloc + GUARD * c->esize;
         c->g[1] = c->g_alloc + (GUARD + buf + gap) * c->esize;
     }
-    // halo buffers: recv_left, recv_right, send_left, send_right; each 3 (IB: 21) slots + guards
+    // halo buffers: recv_left, recv_right, send_left, send_right; each 10 (2-step) or 21 (IB)
+    // slots + guards
     {
-        c->halo_slots = c->max_points > 0 ? IB_HALO_SLOTS : HALO_SLOTS;
+        c->halo_slots = c->max_points > 0 ? IB_HALO_SLOTS : SWEEP_HALO_SLOTS;
         const size_t slot = (size_t)(c->halo_slots * rows + 2 * GUARD) * c->esize;
         int rc = alloc_zero(c, (void**)&c->halo_alloc, 4 * slot);
         if (rc) return bail(rc);

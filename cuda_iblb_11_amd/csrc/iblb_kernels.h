@@ -36,16 +36,23 @@ struct FusedArgs {
 };
 
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.
-// 2-step halo of a slab (9 planes per side, slots of L.rows elements):
-//   from the left  neighbour: 0-2 col -1 {1,5,8}, 3-5 col -1 {0,2,4}, 6-8 col -2 {1,5,8}
-//   from the right neighbour: 0-2 col ncol {3,6,7}, 3-5 col ncol {0,2,4}, 6-8 col ncol+1 {3,6,7}
-// (slots 0-2 are the one-step halo, so a one-step launch can follow a two-step exchange).
-constexpr int SWEEP_HALO_SLOTS = 9;
+// 2-step halo of a slab (SWEEP_HALO_SLOTS slots of L.rows elements per side):
+//   from the left  neighbour: 0-2 col -1 {1,5,8}, 3-5 col -1 {0,2,4}, 6-8 col -2 {1,5,8},
+//                             9: [0] col -1 plane 7 at y = 0, [1] col -1 plane 6 at y = Y-1
+//   from the right neighbour: 0-2 col ncol {3,6,7}, 3-5 col ncol {0,2,4}, 6-8 col ncol+1 {3,6,7},
+//                             9: [0] col ncol plane 8 at y = 0, [1] col ncol plane 5 at y = Y-1
+// (slot 9: the same-cell wall values of the halo column's own collide).  Slots 0-2 are the
+// one-step halo, so a one-step launch can follow a two-step exchange.
+constexpr int SWEEP_HALO_SLOTS = 10;
 // slot of plane k of the d-th column beyond the slab edge (d = 0, 1) in the left / right 2-step
 // halo (-1: not carried)
 __host__ __device__ constexpr int sweep_slot(bool left, int d, int k) {
     return (left ? cx(k) == 1 : cx(k) == -1) ? (d == 0 ? halo_slot(k) : 6 + halo_slot(k))
                                              : (d == 0 && cx(k) == 0 ? 3 + (k == 0 ? 0 : (k == 2 ? 1 : 2)) : -1);
+}
+// plane carried in slot s (< 9) of the halo sent to the left (my columns 0, 1) / right neighbour
+__host__ __device__ constexpr int sweep_send_plane(bool to_left, int s) {
+    return (s >= 3 && s < 6) ? 2 * (s - 3) : (to_left ? right_plane(s % 3) : left_plane(s % 3));
 }
 
 template <typename T>
@@ -53,24 +60,31 @@ struct Sweep2Args {
     const T* src;        // g^t
     T* dst;              // g^{t+2} (the other buffer)
     Layout L;
-    const T* recv_left;  // 2-step halos received from the neighbours; nullptr: single slab
-    const T* recv_right; //   (columns -2, -1, ncol, ncol+1 are the periodic images)
-    T* send_left;        // 2-step halo for the left neighbour (SWEEP_HALO_SLOTS slots), or nullptr
-    T* send_right;
-    int col_begin;       // output columns [col_begin, col_begin + ncols)
-    int ncols;
+    const T* recv_left;  // slab of a group: 2-step halos received from the neighbours
+    const T* recv_right; // (lone slab: columns -2, -1, ncol, ncol+1 are the periodic images)
+    T* send_left;        // slab of a group: 2-step halos for the neighbours, written by the waves
+    T* send_right;       //   of columns 0, 1 / ncol-2, ncol-1
+    int col_begin;       // sweep s covers output columns [col_begin + s*col_step, + W) ∩ [.., col_end)
+    int col_step;
+    int col_end;
+    int nsweep;
     int W;               // output columns per sweep (wave)
     int vs;              // cells per lane; rows, col and plane multiples of vs
-    int nch, nsweep;     // set by launch_sweep2
-    int variant;         // MODE bits (nontemporal loads / stores)
+    int nch;             // set by launch_sweep2
+    int variant;         // MODE bits (nontemporal loads / stores, no prefetch)
     int flux_col;        // local column sampled for Q (both iterations), or -1
     double flux_norm;
     double* Q;
     Coef c;
 };
 
+// slab: true = the group kernel (halo columns from recv_*, send buffers written); false = lone
+// slab (periodic images) or interior columns of a group slab (no halo, no sends)
 template <typename T>
-hipError_t launch_sweep2(Sweep2Args<T> a, hipStream_t s);
+hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s);
+// The 2-step halo of state g into both send buffers (after a one-step launch or an IB exchange).
+template <typename T>
+hipError_t launch_pack_sweep_halo(const T* g, Layout L, T* send_left, T* send_right, hipStream_t st);
 
 // Launch geometry of the collide-stream kernel: one wave per (column, 64*V-row chunk).
 inline int chunks_per_column(int ny, int V) { return (ny + 64 * V - 1) / (64 * V); }

@@ -28,15 +28,31 @@
 
 namespace iblb {
 
+enum { MODE_NO_PREFETCH = 8 };  // sweep only (MODE bits 1, 2 as in lbm_vec.h)
+
 namespace {
 
 // pointer to plane k of column x (x in [-2, ncol+1]); x is wave-uniform.  Computed, not looked
 // up: a table of halo pointers in the kernel arguments costs more SGPRs than a wave has.
-template <typename T>
+template <typename T, bool SLAB>
 __device__ __forceinline__ const T* sweep_col(const Sweep2Args<T>& a, int x, int k) {
     const Layout& L = a.L;
-    const int xw = x < 0 ? x + L.ncol : (x >= L.ncol ? x - L.ncol : x);  // single slab: periodic image
-    return a.src + (long)xw * L.col + (long)k * L.plane;
+    if (x >= 0 && x < L.ncol) return a.src + (long)x * L.col + (long)k * L.plane;
+    if (!SLAB) {  // lone slab: periodic image
+        const int xw = x < 0 ? x + L.ncol : x - L.ncol;
+        return a.src + (long)xw * L.col + (long)k * L.plane;
+    }
+    if (x < 0) return a.recv_left + (long)sweep_slot(true, -1 - x, k) * L.rows;
+    return a.recv_right + (long)sweep_slot(false, x - L.ncol, k) * L.rows;
+}
+
+// g0(x, y, k) for the wall cells (y = 0 or Y-1) of column x; a group slab's halo columns carry
+// the same-cell values their walls need in slot 9
+template <typename T, bool SLAB>
+__device__ __forceinline__ T wall_val(const Sweep2Args<T>& a, int x, int k, int y) {
+    if (SLAB && x == -1 && (k == 7 || k == 6)) return a.recv_left[9 * a.L.rows + (y == 0 ? 0 : 1)];
+    if (SLAB && x == a.L.ncol && (k == 8 || k == 5)) return a.recv_right[9 * a.L.rows + (y == 0 ? 0 : 1)];
+    return sweep_col<T, SLAB>(a, x, k)[y];
 }
 
 // rows y0 .. y0+VS-1 of plane pointer p shifted by one row: DIR = +1 -> rows y-1, DIR = -1 ->
@@ -101,12 +117,12 @@ struct Raw {
 };
 
 // rows of the wave start at row0 = cs - VS (uniform); lane byte offset off
-template <typename T, int VS, int MODE>
+template <typename T, int VS, int MODE, bool SLAB>
 __device__ __forceinline__ void load_raw(const Sweep2Args<T>& a, int x, int row0, unsigned off, bool bot, bool top,
                                          Raw<T, VS>& r) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
-        const T* p = sweep_col<T>(a, x - cx(k), k) + row0;
+        const T* p = sweep_col<T, SLAB>(a, x - cx(k), k) + row0;
         ld_rows<T, VS, MODE>(p, off, r.v[k]);
         // the ghost lanes' own pulls reach one row beyond the wave (uniform address)
         if (cy(k) == 1) r.e[k] = p[-1];
@@ -114,12 +130,12 @@ __device__ __forceinline__ void load_raw(const Sweep2Args<T>& a, int x, int row0
     }
     r.w[0] = r.w[1] = r.w[2] = r.w[3] = (T)0;
     if (bot) {
-        r.w[0] = sweep_col<T>(a, x, 7)[0];
-        r.w[1] = sweep_col<T>(a, x, 8)[0];
+        r.w[0] = wall_val<T, SLAB>(a, x, 7, 0);
+        r.w[1] = wall_val<T, SLAB>(a, x, 8, 0);
     }
     if (top) {
-        r.w[2] = sweep_col<T>(a, x, 5)[a.L.ny - 1];
-        r.w[3] = sweep_col<T>(a, x, 6)[a.L.ny - 1];
+        r.w[2] = wall_val<T, SLAB>(a, x, 5, a.L.ny - 1);
+        r.w[3] = wall_val<T, SLAB>(a, x, 6, a.L.ny - 1);
     }
 }
 
@@ -163,7 +179,7 @@ __device__ __forceinline__ void pull_window(const T (*pk[9])[VS], const T* edge,
 // the chunk's 62*VS output rows [cs, cs + 62*VS), lanes 0 and 63 are ghost rows (the g1 values
 // of the rows just outside the chunk that step 2 pulls).  Ghost rows and rows >= ny compute
 // garbage that no owned row reads.
-template <typename T, int VS, int MODE>
+template <typename T, int VS, int MODE, bool SLAB>
 __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
     typedef typename Calc<T>::R R;
     static_assert(sizeof(R) == sizeof(T), "the window keeps g1 in the storage type");
@@ -174,8 +190,8 @@ __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
     const Layout L = a.L;
     const int sw = gw / a.nch;
     const int ch = gw - sw * a.nch;
-    const int xa = a.col_begin + sw * a.W;
-    const int xb = min(xa + a.W, a.col_begin + a.ncols);
+    const int xa = a.col_begin + sw * a.col_step;
+    const int xb = min(xa + a.W, a.col_end);
     const int cs = ch * (62 * VS);
     const int row0 = cs - VS;  // first row of the wave (lane 0)
     const int r0 = row0 + lane * VS;
@@ -194,11 +210,18 @@ __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
         for (int e = 0; e < VS; ++e) { A[k][e] = 0; B[k][e] = 0; }
     double q = 0.;
 
+    // software prefetch of the next column (MODE_NO_PREFETCH: load at use, fewer VGPRs)
+    constexpr bool PF = !(MODE & MODE_NO_PREFETCH);
     Raw<T, VS> nxt;
-    load_raw<T, VS, MODE>(a, xa - 1, row0, off, bot, top, nxt);
+    if (PF) load_raw<T, VS, MODE, SLAB>(a, xa - 1, row0, off, bot, top, nxt);
     for (int x = xa - 1; x <= xb; ++x) {
-        const Raw<T, VS> cur = nxt;
-        load_raw<T, VS, MODE>(a, min(x + 1, xb), row0, off, bot, top, nxt);
+        Raw<T, VS> cur;
+        if (PF) {
+            cur = nxt;
+            load_raw<T, VS, MODE, SLAB>(a, min(x + 1, xb), row0, off, bot, top, nxt);
+        } else {
+            load_raw<T, VS, MODE, SLAB>(a, x, row0, off, bot, top, cur);
+        }
 
         // ---- step 1: g1[x] ----
         T C[9][VS];
@@ -247,6 +270,35 @@ __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
                 T* dst = a.dst + (long)xo * L.col + row0;
 #pragma unroll
                 for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * L.plane, off, s[k]);
+                if (SLAB) {  // the 2-step halo of g^{t+2} for the neighbours (iblb_kernels.h)
+                    const bool sl0 = xo == 0, sl1 = xo == 1, sr0 = xo == L.ncol - 1, sr1 = xo == L.ncol - 2;
+                    if (sl0 || sl1 || sr0 || sr1) {
+                        T* buf = (sl0 || sl1) ? a.send_left + row0 : a.send_right + row0;
+                        const bool left = sl0 || sl1;
+                        const int s0 = (sl0 || sr0) ? 0 : 6;
+                        const int ns = (sl0 || sr0) ? 6 : 3;
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) {
+                            if (q >= ns) break;
+                            const int sl = s0 + q;
+                            // slot sl carries plane sweep_send_plane(left, sl)
+                            T v[VS];
+#pragma unroll
+                            for (int k = 0; k < 9; ++k)
+                                if (k == (left ? sweep_send_plane(true, sl) : sweep_send_plane(false, sl)))
+#pragma unroll
+                                    for (int e = 0; e < VS; ++e) v[e] = s[k][e];
+                            st_rows<T, VS, 0>(buf + (long)sl * L.rows, off, v);
+                        }
+                        if (sl0 || sr0) {  // slot 9: the same-cell wall values of this column
+                            T* w = buf - row0 + 9 * L.rows;
+                            if (bot) w[0] = sl0 ? s[8][0] : s[7][0];
+#pragma unroll
+                            for (int e = 0; e < VS; ++e)
+                                if (top && e == et) w[1] = sl0 ? s[5][e] : s[6][e];
+                        }
+                    }
+                }
             }
         }
 
@@ -263,39 +315,76 @@ __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
 }
 
 template <typename T, int VS, int MODE>
-static hipError_t launch_sweep_mode(const Sweep2Args<T>& a, unsigned blocks, hipStream_t s) {
-    sweep2_kernel<T, VS, MODE><<<blocks, 256, 0, s>>>(a);
+static hipError_t launch_sweep_mode(const Sweep2Args<T>& a, bool slab, unsigned blocks, hipStream_t s) {
+    if (slab) sweep2_kernel<T, VS, MODE, true><<<blocks, 256, 0, s>>>(a);
+    else sweep2_kernel<T, VS, MODE, false><<<blocks, 256, 0, s>>>(a);
     return hipGetLastError();
 }
 
 template <typename T, int VS>
-static hipError_t launch_sweep_vs(const Sweep2Args<T>& a, unsigned blocks, hipStream_t s) {
+static hipError_t launch_sweep_vs(const Sweep2Args<T>& a, bool slab, unsigned blocks, hipStream_t s) {
     switch (a.variant) {
-        case 1: return launch_sweep_mode<T, VS, 1>(a, blocks, s);
-        case 2: return launch_sweep_mode<T, VS, 2>(a, blocks, s);
-        case 3: return launch_sweep_mode<T, VS, 3>(a, blocks, s);
-        default: return launch_sweep_mode<T, VS, 0>(a, blocks, s);
+        case 1: return launch_sweep_mode<T, VS, 1>(a, slab, blocks, s);
+        case 2: return launch_sweep_mode<T, VS, 2>(a, slab, blocks, s);
+        case 3: return launch_sweep_mode<T, VS, 3>(a, slab, blocks, s);
+        case 8: return launch_sweep_mode<T, VS, 8>(a, slab, blocks, s);
+        case 9: return launch_sweep_mode<T, VS, 9>(a, slab, blocks, s);
+        default: return launch_sweep_mode<T, VS, 0>(a, slab, blocks, s);
     }
 }
 
 template <typename T>
-hipError_t launch_sweep2(Sweep2Args<T> a, hipStream_t s) {
-    if (a.ncols <= 0) return hipSuccess;
-    // rows are read up to VS below 0 and nch*62*VS + VS - 1 (< rows + 62*VS + VS): inside the
-    // 512-element guards of the buffers (iblb_ctx.hip)
+hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s) {
+    if (a.nsweep <= 0) return hipSuccess;
+    // rows are read up to VS+1 below 0 and up to nch*62*VS + VS (< rows + 62*VS + VS + 1): inside
+    // the 512-element guards of the buffers (iblb_ctx.hip)
     if (a.W <= 0 || a.L.ncol < 2 || a.vs <= 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 || a.L.col % a.vs != 0)
         return hipErrorInvalidValue;
+    if (slab && (!a.recv_left || !a.recv_right || !a.send_left || !a.send_right)) return hipErrorInvalidValue;
     a.nch = (a.L.ny + 62 * a.vs - 1) / (62 * a.vs);
-    a.nsweep = (a.ncols + a.W - 1) / a.W;
     const long waves = (long)a.nsweep * a.nch;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     constexpr int V = vec_of<T>();
-    if (a.vs == V) return launch_sweep_vs<T, V>(a, blocks, s);
-    if (a.vs == V / 2) return launch_sweep_vs<T, V / 2>(a, blocks, s);
+    if (a.vs == V) return launch_sweep_vs<T, V>(a, slab, blocks, s);
+    if (a.vs == V / 2) return launch_sweep_vs<T, V / 2>(a, slab, blocks, s);
     return hipErrorInvalidValue;
 }
 
-template hipError_t launch_sweep2<double>(Sweep2Args<double>, hipStream_t);
-template hipError_t launch_sweep2<float>(Sweep2Args<float>, hipStream_t);
+// 2-step halo of g into the send buffers (slot layout in iblb_kernels.h); one thread per
+// (side, slot, row)
+template <typename T>
+__global__ void pack_sweep_halo_kernel(const T* __restrict__ g, Layout L, T* __restrict__ sl, T* __restrict__ sr) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long per_side = 9L * L.ny + 2;
+    if (idx >= 2 * per_side) return;
+    const bool left = idx < per_side;
+    const long i = left ? idx : idx - per_side;
+    T* buf = left ? sl : sr;
+    const int c0 = left ? 0 : L.ncol - 1;
+    if (i >= 9L * L.ny) {  // slot 9: wall values of the edge column
+        const int w = (int)(i - 9L * L.ny);
+        const int k = w == 0 ? (left ? 8 : 7) : (left ? 5 : 6);
+        const int y = w == 0 ? 0 : L.ny - 1;
+        buf[9 * L.rows + w] = g[(long)c0 * L.col + (long)k * L.plane + y];
+        return;
+    }
+    const int sl_ = (int)(i / L.ny), y = (int)(i - (long)sl_ * L.ny);
+    const int col = sl_ < 6 ? c0 : (left ? 1 : L.ncol - 2);
+    const int k = sweep_send_plane(left, sl_);
+    buf[(long)sl_ * L.rows + y] = g[(long)col * L.col + (long)k * L.plane + y];
+}
+
+template <typename T>
+hipError_t launch_pack_sweep_halo(const T* g, Layout L, T* send_left, T* send_right, hipStream_t st) {
+    if (L.ncol < 2) return hipErrorInvalidValue;
+    const long n = 2 * (9L * L.ny + 2);
+    pack_sweep_halo_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(g, L, send_left, send_right);
+    return hipGetLastError();
+}
+
+template hipError_t launch_pack_sweep_halo<double>(const double*, Layout, double*, double*, hipStream_t);
+template hipError_t launch_pack_sweep_halo<float>(const float*, Layout, float*, float*, hipStream_t);
+template hipError_t launch_sweep2<double>(Sweep2Args<double>, bool, hipStream_t);
+template hipError_t launch_sweep2<float>(Sweep2Args<float>, bool, hipStream_t);
 
 }  // namespace iblb

@@ -4,7 +4,10 @@ iblb_step / readers) with N ranks as threads on one GPU, through the mock-RCCL b
 (tests/mock_rccl/libiblb_mockrccl.so), and compare with a single-slab context of the same
 build.  Prints one JSON line; exit status 0 = match.
 
-usage: run_group.py NRANKS NX NY STEPS WITH_IB(0/1) PRECISION(f64/f32)
+usage: run_group.py NRANKS NX NY STEPS WITH_IB(0/1) PRECISION(f64/f32) [BULK(0/1)]
+
+BULK=1 (no IB): the group advances in multi-step calls (two-iteration sweeps with the 2-step
+halo, one-step launches for odd remainders) instead of one iteration per call.
 """
 import json
 import os
@@ -25,6 +28,7 @@ from cuda_iblb_11_amd.lattice import Lattice, plan_slabs, rccl_unique_id, split_
 def main():
     n, nx, ny, steps, with_ib, prec = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]),
                                         sys.argv[5] == "1", sys.argv[6])
+    bulk = len(sys.argv) > 7 and sys.argv[7] == "1" and not with_ib
     lib = L.load_from(os.path.join(HERE, "libiblb_mockrccl.so"))
     rho, u = W.perturbed_state(nx, ny, 31)
     bf = (1e-6, 2e-7)
@@ -72,7 +76,16 @@ def main():
                       x_count=xc, lib=lib)
         lat.set_state(split_state(rho, 1, nx, ny, xb, xc), split_state(u, 2, nx, ny, xb, xc))
         lat.attach_rccl(uid, n, r)
-        for it in range(steps):
+        if bulk:  # calls of 3, 1, 2, ... steps up to the checkpoint, the rest in one call
+            t = 0
+            for k in (3, 1, 2, 4):
+                if t + k <= half:
+                    lat.step(k)
+                    t += k
+            lat.step(half - t)
+            lat.save_checkpoint(ck(r))
+            lat.step(steps - half)
+        for it in range(0 if not bulk else steps, steps):
             if it == half:
                 lat.save_checkpoint(ck(r))
             if with_ib:
@@ -92,7 +105,9 @@ def main():
                       x_count=xc, lib=lib)
         lat.attach_rccl(uid2, n, r)
         lat.load_checkpoint(ck(r))
-        for it in range(half, steps):
+        if bulk:
+            lat.step(steps - half)
+        for it in range(half if not bulk else steps, steps):
             if with_ib:
                 lat.set_lagrangian(*pts(it))
             lat.step(1)

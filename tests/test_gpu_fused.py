@@ -264,21 +264,24 @@ def test_errors_are_loud(gpu):
         slab.step(1)  # slab not linked to neighbours
 
 
-@pytest.mark.parametrize("n,with_ib,precision,overlap", [(2, False, "f64", 1), (3, False, "f64", 1),
-                                                         (3, False, "f64", 0), (2, True, "f64", 1),
-                                                         (4, True, "f64", 1), (2, False, "f32", 1)])
-def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap):
+@pytest.mark.parametrize("n,with_ib,precision,overlap,bulk", [(2, False, "f64", 1, 0), (3, False, "f64", 1, 0),
+                                                              (3, False, "f64", 0, 0), (2, True, "f64", 1, 0),
+                                                              (4, True, "f64", 1, 0), (2, False, "f32", 1, 0),
+                                                              (2, False, "f64", 1, 1), (3, False, "f64", 1, 1),
+                                                              (3, False, "f64", 0, 1), (4, False, "f32", 1, 1)])
+def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap, bulk):
     """The RCCL transport of iblb_ctx.hip (attach, halo send/recv pairing, node-value and
     flux all-reduces, collective readers) driven with N ranks as threads on the one GPU via
     the mock-RCCL test build (RCCL itself refuses two ranks on one device).  Without IB the
-    decomposed run must be bit-identical to one slab."""
+    decomposed run must be bit-identical to one slab; bulk: multi-step calls, i.e. the
+    two-iteration sweeps with the 2-step halo (boundary sweeps on the comm stream)."""
     import json
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     cmd = [sys.executable, os.path.join(here, "mock_rccl", "run_group.py"), str(n), "48", "130", "25",
-           "1" if with_ib else "0", precision]
+           "1" if with_ib else "0", precision, str(bulk)]
     env = dict(os.environ, IBLB_OVERLAP=str(overlap))
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -432,9 +435,10 @@ def test_interleaved_layout_identical(gpu, monkeypatch, precision):
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("overlap", [1, 0])
 def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap):
-    """Bulk stepping of an RCCL group: the two-stream schedule (halo exchange and boundary
-    columns on the comm stream beside the interior launch) over real RCCL (self ring), readers
-    interleaved; must equal the plain single slab bit for bit."""
+    """Bulk stepping of an RCCL group over real RCCL (self ring), readers interleaved: the
+    two-iteration sweeps with the 2-step halo (boundary sweeps on the comm stream beside the
+    interior sweep) and one-step launches for odd remainders; must equal the plain single slab
+    bit for bit."""
     from cuda_iblb_11_amd import workloads as W
     monkeypatch.setenv("IBLB_RCCL_SELF", "1")
     monkeypatch.setenv("IBLB_OVERLAP", str(overlap))
@@ -445,6 +449,7 @@ def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap):
     ref.set_state(rho, u)
     ring.set_state(rho, u)
     ring.attach_rccl(gpu.rccl_unique_id(), 1, 0)
+    ring.set_profiling(True)
     for n in (3, 37, 1, 2, 64):
         ref.step(n)
         ring.step(n)
@@ -453,6 +458,7 @@ def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap):
         assert np.array_equal(r1, r2) and np.array_equal(u1, u2), n
     assert ring.steps == ref.steps == 107
     assert abs(ring.flux - ref.flux) <= 1e-13 * abs(ref.flux)  # per-chunk atomics: order varies
+    assert ring.timing()["sweep_launches"] >= 40  # the interior sweeps ran
     ring.close()
 
 
