@@ -185,11 +185,24 @@ __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
     static_assert(sizeof(R) == sizeof(T), "the window keeps g1 in the storage type");
     constexpr bool DEV = Store<T>::dev;
     const int lane = threadIdx.x & 63;
-    const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (gw >= a.nsweep * a.nch) return;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int sw, ch;
+    if (a.map == 0) {
+        // a workgroup = 4 neighbouring sweeps of one chunk (their shared edge columns are read
+        // once from HBM), workgroups remapped so that each XCD (blocks b = 8*slot + xcd) walks a
+        // contiguous range of (chunk, sweep group): neighbouring groups run on one L2
+        const int nb = (int)gridDim.x, b = (int)blockIdx.x, q = nb / 8;
+        const int work = b < 8 * q ? (b % 8) * q + b / 8 : b;
+        const int ngroups = (a.nsweep + 3) / 4;
+        ch = work / ngroups;
+        sw = (work - ch * ngroups) * 4 + wv;
+    } else {  // linear: wave -> (sweep, chunk), chunk fastest
+        const int gw = blockIdx.x * 4 + wv;
+        sw = gw / a.nch;
+        ch = gw - sw * a.nch;
+    }
+    if (sw >= a.nsweep || ch >= a.nch) return;
     const Layout L = a.L;
-    const int sw = gw / a.nch;
-    const int ch = gw - sw * a.nch;
     const int xa = a.col_begin + sw * a.col_step;
     const int xb = min(xa + a.W, a.col_end);
     const int cs = ch * (62 * VS);
@@ -342,8 +355,8 @@ hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s) {
         return hipErrorInvalidValue;
     if (slab && (!a.recv_left || !a.recv_right || !a.send_left || !a.send_right)) return hipErrorInvalidValue;
     a.nch = (a.L.ny + 62 * a.vs - 1) / (62 * a.vs);
-    const long waves = (long)a.nsweep * a.nch;
-    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    const unsigned blocks = a.map == 0 ? (unsigned)(((a.nsweep + 3) / 4) * (long)a.nch)
+                                       : (unsigned)(((long)a.nsweep * a.nch + 3) / 4);
     constexpr int V = vec_of<T>();
     if (a.vs == V) return launch_sweep_vs<T, V>(a, slab, blocks, s);
     if (a.vs == V / 2) return launch_sweep_vs<T, V / 2>(a, slab, blocks, s);
