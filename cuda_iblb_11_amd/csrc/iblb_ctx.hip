@@ -62,7 +62,7 @@ struct iblb_ctx {
     // two iterations per launch (lbm_sweep.hip) where no IB force is owed in between:
     // IBLB_SWEEP (on), IBLB_SWEEP_W columns per wave, IBLB_SWEEP_VS cells per lane, variant
     bool sweep_on = true;
-    int sweep_w = 4, sweep_vs = 2, sweep_variant = 1, sweep_map = 1;
+    int sweep_w = 4, sweep_vs = 2, sweep_variant = 1, sweep_map = 2, sweep_alt = 1;
     hipStream_t stream = nullptr;
     Coef coef{};
     // populations: two buffers in one allocation (deterministic relative placement of the
@@ -466,6 +466,7 @@ Sweep2Args<T> sweep_args(iblb_ctx* c, int col_begin, int col_step, int col_end, 
     a.vs = c->sweep_vs;
     a.variant = c->sweep_variant;
     a.map = c->sweep_map;
+    a.alt = c->sweep_alt;
     const int fc = c->cfg.flux_column - c->x_begin;
     a.flux_col = (fc >= 0 && fc < c->ncol) ? fc : -1;
     a.flux_norm = c->cfg.flux_norm;
@@ -718,14 +719,17 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     // loads and stores (3; 0.193 ms vs 0.218 ms planar variant 2, profiles/r01e_tune_f32.log)
     c->variant = (int)env_long("IBLB_FUSED_VARIANT", c->prec == IBLB_PREC_F64 ? 5 : 3);
     c->sweep_on = env_long("IBLB_SWEEP", 1) != 0;
-    // measured on MI355X (profiles/r01p_tune_*.log, r01q_tune_*.log): 16 B per lane (f64 2 cells,
-    // f32 4), short sweeps (f64 4 columns: 4096^2 0.233 ms/iteration vs 0.406 one-step, 512 x 4096
-    // 0.036 vs 0.061; f32 6 columns: 0.124 vs 0.199), nontemporal stores, linear wave order (the
-    // XCD-contiguous 4-sweep workgroups, IBLB_SWEEP_MAP=0, measured 10-15 % slower)
+    // measured on MI355X (profiles/r01p_tune_*.log, r01q_*, r01s_*, r01t_*): 16 B per lane (f64 2
+    // cells, f32 4), short sweeps (f64 4 columns: 4096^2 0.227 ms/iteration vs 0.406 one-step,
+    // 512 x 4096 0.034 vs 0.061; f32 6 columns: 0.118 vs 0.199), nontemporal stores, the linear
+    // wave order dealt to the XCDs in contiguous ranges (map 2, 4 % faster than plain linear) with
+    // alternate sweeps walking towards each other (alt: HBM fetch 1.08x the state instead of
+    // 1.38x / 1.60x); the XCD-contiguous 4-sweep workgroups (map 0) measured 10-15 % slower
     c->sweep_w = (int)env_long("IBLB_SWEEP_W", c->prec == IBLB_PREC_F64 ? 4 : 6);
     c->sweep_vs = (int)env_long("IBLB_SWEEP_VS", c->prec == IBLB_PREC_F64 ? 2 : 4);
     c->sweep_variant = (int)env_long("IBLB_SWEEP_VARIANT", 1);
-    c->sweep_map = (int)env_long("IBLB_SWEEP_MAP", 1);
+    c->sweep_map = (int)env_long("IBLB_SWEEP_MAP", 2);
+    c->sweep_alt = (int)env_long("IBLB_SWEEP_ALT", 1);
     if (c->cfg.flux_column < 0) c->cfg.flux_column = c->nx - 5;
 
     const double tau = cfg->tau, tau2 = cfg->tau2, cs = 0.57735;
@@ -1327,8 +1331,14 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
         const int prio = env_long("IBLB_COMM_PRIORITY", 1) != 0 ? prio_hi : prio_lo;
         HIP_TRY(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming));
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_int, hipEventDisableTiming));
+        // cross-stream ordering events (producer and consumer on this device): IBLB_EVENT_FENCE
+        // 0 = HIP's default system-scope release / acquire, 1 = hipEventDisableSystemFence,
+        // 2 = hipEventReleaseToDevice
+        const long ef = env_long("IBLB_EVENT_FENCE", 0);
+        const unsigned evf = hipEventDisableTiming |
+                             (ef == 1 ? hipEventDisableSystemFence : (ef == 2 ? hipEventReleaseToDevice : 0u));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, evf));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_int, evf));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;

@@ -72,7 +72,9 @@ struct Sweep2Args {
     int vs;              // cells per lane; rows, col and plane multiples of vs
     int nch;             // set by launch_sweep2
     int variant;         // MODE bits (nontemporal loads / stores, no prefetch)
-    int map;             // 1: linear, chunk fastest (default); 0: 4 sweeps per workgroup, XCD-contiguous
+    int map;             // 1: linear, chunk fastest; 0: 4 sweeps per workgroup, XCD-contiguous;
+                         // 2: linear order in XCD-contiguous ranges (default)
+    int alt;             // odd sweeps walk right to left (neighbours read their shared edges together)
     int flux_col;        // local column sampled for Q (both iterations), or -1
     double flux_norm;
     double* Q;

@@ -175,47 +175,22 @@ __device__ __forceinline__ void pull_window(const T (*pk[9])[VS], const T* edge,
 
 }  // namespace
 
-// One wave = (sweep, chunk).  Lane l holds rows r0 = cs - VS + l*VS .. r0+VS-1: lanes 1..62 own
-// the chunk's 62*VS output rows [cs, cs + 62*VS), lanes 0 and 63 are ghost rows (the g1 values
-// of the rows just outside the chunk that step 2 pulls).  Ghost rows and rows >= ny compute
-// garbage that no owned row reads.
-template <typename T, int VS, int MODE, bool SLAB>
-__global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
+// The walk of one wave over the output columns [xa, xb): step 1 makes g1 of columns xa-1 .. xb
+// in walking order, step 2 makes g2 of the middle column of the last three.  REV walks from xb
+// down to xa-1 (the window mirrored: A = g1[x+2], C = g1[x]); alternate sweeps walking towards
+// each other read their shared edge columns at the same time, so one fetch serves both.
+// Returns this lane's flux partial.
+template <typename T, int VS, int MODE, bool SLAB, bool REV>
+__device__ __forceinline__ double sweep_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
+                                             int lane, int r0, int et, bool owner, bool bot, bool top) {
     typedef typename Calc<T>::R R;
-    static_assert(sizeof(R) == sizeof(T), "the window keeps g1 in the storage type");
     constexpr bool DEV = Store<T>::dev;
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int sw, ch;
-    if (a.map == 0) {
-        // a workgroup = 4 neighbouring sweeps of one chunk (their shared edge columns are read
-        // once from HBM), workgroups remapped so that each XCD (blocks b = 8*slot + xcd) walks a
-        // contiguous range of (chunk, sweep group): neighbouring groups run on one L2
-        const int nb = (int)gridDim.x, b = (int)blockIdx.x, q = nb / 8;
-        const int work = b < 8 * q ? (b % 8) * q + b / 8 : b;
-        const int ngroups = (a.nsweep + 3) / 4;
-        ch = work / ngroups;
-        sw = (work - ch * ngroups) * 4 + wv;
-    } else {  // linear: wave -> (sweep, chunk), chunk fastest
-        const int gw = blockIdx.x * 4 + wv;
-        sw = gw / a.nch;
-        ch = gw - sw * a.nch;
-    }
-    if (sw >= a.nsweep || ch >= a.nch) return;
     const Layout L = a.L;
-    const int xa = a.col_begin + sw * a.col_step;
-    const int xb = min(xa + a.W, a.col_end);
-    const int cs = ch * (62 * VS);
-    const int row0 = cs - VS;  // first row of the wave (lane 0)
-    const int r0 = row0 + lane * VS;
-    const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
-    const int et = L.ny - 1 - r0;  // element of the top row, if in [0, VS)
-    const bool owner = lane >= 1 && lane <= 62 && r0 < L.ny;
-    const bool bot = r0 == 0;
-    const bool top = et >= 0 && et < VS;
     const double gx = a.c.gx, gy = a.c.gy;
+    // first, last and next column of the walk
+    const int x0 = REV ? xb : xa - 1, x1 = REV ? xa - 1 : xb, dx = REV ? -1 : 1;
 
-    // g1 window: A = g1[x-2] (planes 1, 5, 8 used), B = g1[x-1], C = g1[x]
+    // g1 window: A = g1[x-2dx] (planes with c_x = dx used), B = g1[x-dx], C = g1[x]
     T A[9][VS], B[9][VS];
 #pragma unroll
     for (int k = 0; k < 9; ++k)
@@ -226,12 +201,12 @@ __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
     // software prefetch of the next column (MODE_NO_PREFETCH: load at use, fewer VGPRs)
     constexpr bool PF = !(MODE & MODE_NO_PREFETCH);
     Raw<T, VS> nxt;
-    if (PF) load_raw<T, VS, MODE, SLAB>(a, xa - 1, row0, off, bot, top, nxt);
-    for (int x = xa - 1; x <= xb; ++x) {
+    if (PF) load_raw<T, VS, MODE, SLAB>(a, x0, row0, off, bot, top, nxt);
+    for (int i = 0, x = x0; i <= xb - xa + 1; ++i, x += dx) {
         Raw<T, VS> cur;
         if (PF) {
             cur = nxt;
-            load_raw<T, VS, MODE, SLAB>(a, min(x + 1, xb), row0, off, bot, top, nxt);
+            load_raw<T, VS, MODE, SLAB>(a, x == x1 ? x : x + dx, row0, off, bot, top, nxt);
         } else {
             load_raw<T, VS, MODE, SLAB>(a, x, row0, off, bot, top, cur);
         }
@@ -260,12 +235,13 @@ __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
             }
         }
 
-        // ---- step 2: g2[x-1] from the window ----
-        if (x > xa) {
-            const int xo = x - 1;
+        // ---- step 2: g2[x-dx] from the window ----
+        if (i >= 2) {
+            const int xo = x - dx;
             const T(*pk[9])[VS];
+            // plane k of g2[xo] pulls from g1[xo - c_x(k)]: c_x = dx -> A, c_x = -dx -> C
 #pragma unroll
-            for (int k = 0; k < 9; ++k) pk[k] = cx(k) == 1 ? &A[k] : (cx(k) == -1 ? &C[k] : &B[k]);
+            for (int k = 0; k < 9; ++k) pk[k] = cx(k) == dx ? &A[k] : (cx(k) == -dx ? &C[k] : &B[k]);
             T s[9][VS];
             pull_window<T, VS>(pk, nullptr, B[2], B[4], B[7][0], B[8][0], B[5], B[6], lane, r0, et, s);
             const bool flux2 = xo == a.flux_col;
@@ -321,9 +297,59 @@ __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
 #pragma unroll
             for (int e = 0; e < VS; ++e) { A[k][e] = B[k][e]; B[k][e] = C[k][e]; }
     }
+    return q;
+}
+
+// One wave = (sweep, chunk).  Lane l holds rows r0 = cs - VS + l*VS .. r0+VS-1: lanes 1..62 own
+// the chunk's 62*VS output rows [cs, cs + 62*VS), lanes 0 and 63 are ghost rows (the g1 values
+// of the rows just outside the chunk that step 2 pulls).  Ghost rows and rows >= ny compute
+// garbage that no owned row reads.
+template <typename T, int VS, int MODE, bool SLAB>
+__global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
+    typedef typename Calc<T>::R R;
+    static_assert(sizeof(R) == sizeof(T), "the window keeps g1 in the storage type");
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int sw, ch;
+    if (a.map == 0) {
+        // a workgroup = 4 neighbouring sweeps of one chunk (their shared edge columns are read
+        // once from HBM), workgroups remapped so that each XCD (blocks b = 8*slot + xcd) walks a
+        // contiguous range of (chunk, sweep group): neighbouring groups run on one L2
+        const int nb = (int)gridDim.x, b = (int)blockIdx.x, q = nb / 8;
+        const int work = b < 8 * q ? (b % 8) * q + b / 8 : b;
+        const int ngroups = (a.nsweep + 3) / 4;
+        ch = work / ngroups;
+        sw = (work - ch * ngroups) * 4 + wv;
+    } else {
+        // linear: wave -> (sweep, chunk), chunk fastest.  map 2: the same order dealt to the
+        // XCDs in contiguous ranges (blocks b and b+8 share an XCD), so the edge columns of
+        // neighbouring sweeps are re-read from the L2 that just fetched them
+        int b = (int)blockIdx.x;
+        if (a.map == 2) {
+            const int q = (int)gridDim.x / 8;
+            if (b < 8 * q) b = (b % 8) * q + b / 8;
+        }
+        const int gw = b * 4 + wv;
+        sw = gw / a.nch;
+        ch = gw - sw * a.nch;
+    }
+    if (sw >= a.nsweep || ch >= a.nch) return;
+    const int xa = a.col_begin + sw * a.col_step;
+    const int xb = min(xa + a.W, a.col_end);
+    const int cs = ch * (62 * VS);
+    const int row0 = cs - VS;  // first row of the wave (lane 0)
+    const int r0 = row0 + lane * VS;
+    const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
+    const int et = a.L.ny - 1 - r0;  // element of the top row, if in [0, VS)
+    const bool owner = lane >= 1 && lane <= 62 && r0 < a.L.ny;
+    const bool bot = r0 == 0;
+    const bool top = et >= 0 && et < VS;
+    const double q = (a.alt && (sw & 1))
+                         ? sweep_walk<T, VS, MODE, SLAB, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
+                         : sweep_walk<T, VS, MODE, SLAB, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top);
     if (a.flux_col >= xa && a.flux_col < xb) {
-        q = wave_sum(q);
-        if (lane == 0) atomicAdd(a.Q, q);
+        const double qs = wave_sum(q);
+        if (lane == 0) atomicAdd(a.Q, qs);
     }
 }
 

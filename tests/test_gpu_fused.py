@@ -466,7 +466,7 @@ def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap):
 def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch):
     """The two-iteration sweep kernel (g1 kept in registers, ghost lanes for the chunk edges,
     periodic columns) equals pairs of one-step launches bit for bit, for every cells-per-lane
-    width, sweep length, load/store/prefetch variant and wave mapping, on shapes with ragged chunks (ny not a multiple of
+    width, sweep length, load/store/prefetch variant, wave mapping and walking direction, on shapes with ragged chunks (ny not a multiple of
     62*VS), fewer columns than one sweep, one-row-above-a-chunk tops and several chunks; odd step
     counts end with a one-step launch.  Flux: same terms, other summation order."""
     from cuda_iblb_11_amd import workloads as W
@@ -481,13 +481,15 @@ def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch)
         ref.close()
         monkeypatch.setenv("IBLB_SWEEP", "1")
         for vs in vss:
-            for w, var, mp in [(1, 0, 0), (3, 1, 0), (32, 2, 0), (8, 3, 0), (3, 8, 0), (5, 9, 0), (1, 1, 1),
-                               (7, 9, 1), (32, 1, 1)]:
+            for w, var, mp, alt in [(1, 0, 0, 0), (3, 1, 0, 1), (32, 2, 0, 0), (8, 3, 0, 0), (3, 8, 0, 1),
+                                    (5, 9, 0, 0), (1, 1, 1, 1), (7, 9, 1, 0), (32, 1, 1, 0), (4, 1, 2, 0),
+                                    (4, 1, 2, 1), (1, 9, 2, 1), (6, 8, 1, 1)]:
                 if True:
                     monkeypatch.setenv("IBLB_SWEEP_VS", str(vs))
                     monkeypatch.setenv("IBLB_SWEEP_W", str(w))
                     monkeypatch.setenv("IBLB_SWEEP_VARIANT", str(var))
                     monkeypatch.setenv("IBLB_SWEEP_MAP", str(mp))
+                    monkeypatch.setenv("IBLB_SWEEP_ALT", str(alt))
                     lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 3e-7))
                     lat.set_state(rho, u)
                     lat.set_profiling(True)
@@ -495,10 +497,10 @@ def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch)
                     tm = lat.timing()
                     assert tm["sweep_launches"] == 15 and tm["fused_launches"] == 1, tm
                     f = lat.populations()
-                    assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, mp, float(np.max(np.abs(f - f_ref))))
+                    assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, mp, alt, float(np.max(np.abs(f - f_ref))))
                     assert abs(lat.flux - q_ref) <= 1e-12 * abs(q_ref), (lat.flux, q_ref)
                     lat.close()
-    for name in ("IBLB_SWEEP_VS", "IBLB_SWEEP_W", "IBLB_SWEEP_VARIANT", "IBLB_SWEEP_MAP"):
+    for name in ("IBLB_SWEEP_VS", "IBLB_SWEEP_W", "IBLB_SWEEP_VARIANT", "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT"):
         monkeypatch.delenv(name)
     lat, sim = run_pair(gpu, oracle, 70, 125, 40, precision=precision)
     check_fields(lat, sim, TIGHT if precision == "f64" else TOL32)
