@@ -116,7 +116,9 @@ struct iblb_ctx {
     hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with the interior
     hipEvent_t ev_bnd = nullptr;  // boundary columns + send buffers of the state written (either stream)
     hipEvent_t ev_int = nullptr;  // compute-stream work of the last step done
+    hipEvent_t ev_pre = nullptr;  // compute-stream work before the interior sweep (sweep order 1)
     bool overlap = true;
+    int sweep_order = 0;          // IBLB_SWEEP_ORDER: 1 = the host submits the interior sweep first
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -511,13 +513,31 @@ int sweep_step(iblb_ctx* c) {
     }
     const bool ov = c->overlap;
     hipStream_t bs = ov ? c->comm_stream : c->stream;
+    const int ni = c->ncol - 4;  // interior [2, ncol-2): needs nothing from the halo
+    if (ov && c->sweep_order == 1) {
+        // the same dependencies, submitted interior first: the launch the step time depends on
+        // leaves the host before the RCCL group and the boundary launch (whose host cost then
+        // overlaps the interior); boundary(t) waits for ev_pre = the compute work before
+        // interior(t), i.e. interior(t-2), which read the columns it overwrites
+        HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
+        if (ni > 0 && (rc = sweep_launch<T>(c, sweep_args<T>(c, 2, W, c->ncol - 2, (ni + W - 1) / W, W), false,
+                                            c->stream, true, (long long)ni * c->ny)))
+            return rc;
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        if ((rc = exchange_rccl(c, bs, false, true))) return rc;
+        HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_pre, 0));
+        if ((rc = sweep_launch<T>(c, sweep_args<T>(c, 0, c->ncol - 2, c->ncol, 2, 2), true, bs, false, 0))) return rc;
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
+        after_sweep(c);
+        c->send_sweep = true;
+        return IBLB_OK;
+    }
     if (!ov) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
     if ((rc = exchange_rccl(c, bs, false, true))) return rc;
     if (ov) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
     // boundary sweeps: [0, 2) and [ncol-2, ncol)
     if ((rc = sweep_launch<T>(c, sweep_args<T>(c, 0, c->ncol - 2, c->ncol, 2, 2), true, bs, false, 0))) return rc;
     if (ov) HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
-    const int ni = c->ncol - 4;  // interior [2, ncol-2): needs nothing from the halo
     if (ni > 0 && (rc = sweep_launch<T>(c, sweep_args<T>(c, 2, W, c->ncol - 2, (ni + W - 1) / W, W), false, c->stream,
                                         true, (long long)ni * c->ny)))
         return rc;
@@ -818,6 +838,7 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
     if (c->ev_int) (void)hipEventDestroy(c->ev_int);
+    if (c->ev_pre) (void)hipEventDestroy(c->ev_pre);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->g_alloc) (void)hipFree(c->g_alloc);
     void* bufs[] = {c->cil_samples, c->cil_lasts, c->cil_bpoints,
@@ -1339,6 +1360,8 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
                              (ef == 1 ? hipEventDisableSystemFence : (ef == 2 ? hipEventReleaseToDevice : 0u));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, evf));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_int, evf));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_pre, evf));
+        c->sweep_order = (int)env_long("IBLB_SWEEP_ORDER", 0);
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
