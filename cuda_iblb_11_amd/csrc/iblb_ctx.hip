@@ -1353,9 +1353,10 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         const int prio = env_long("IBLB_COMM_PRIORITY", 1) != 0 ? prio_hi : prio_lo;
         HIP_TRY(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
         // cross-stream ordering events (producer and consumer on this device): IBLB_EVENT_FENCE
-        // 0 = HIP's default system-scope release / acquire, 1 = hipEventDisableSystemFence,
-        // 2 = hipEventReleaseToDevice
-        const long ef = env_long("IBLB_EVENT_FENCE", 0);
+        // 0 = HIP's default system-scope release / acquire, 1 = hipEventDisableSystemFence
+        // (default: 512 x 4096 self ring 0.0394 vs 0.0420 ms/iteration, 1024 0.0682 vs 0.0705,
+        // profiles/r01u_gap_probe_event_fence.txt), 2 = hipEventReleaseToDevice
+        const long ef = env_long("IBLB_EVENT_FENCE", 1);
         const unsigned evf = hipEventDisableTiming |
                              (ef == 1 ? hipEventDisableSystemFence : (ef == 2 ? hipEventReleaseToDevice : 0u));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_bnd, evf));
