@@ -3,9 +3,11 @@
 "MLUPS and achieved-HBM-GB/s, 4096^2 D2Q9 channel, 1/2/4/8 MI355X".
 
 One step = one reference iteration (main.cu:852-909) over the whole 4096 x 4096 channel
-(periodic x, bounce-back / mirror walls, TRT + Guo forcing, uniform body force, no IB):
-one fused pull-stream + collide launch per slab.  N > 1: x-slab decomposition of the SAME
-4096^2 lattice (strong scaling), one process per GPU, one-column halo via RCCL.
+(periodic x, bounce-back / mirror walls, TRT + Guo forcing, uniform body force, no IB): one
+two-iteration sweep launch (pull-stream + collide twice, lbm_sweep.hip) per two steps and slab.
+N > 1: x-slab decomposition of the SAME 4096^2 lattice (strong scaling), one process per GPU,
+2-column halo via RCCL beside the interior sweep; `--scaling weak`
+gives every rank the configured width instead ((nx*N) x ny).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f64|f32] [--nx 4096 --ny 4096]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
@@ -65,6 +67,9 @@ def parse():
     p.add_argument("--nx", type=int, default=None)
     p.add_argument("--ny", type=int, default=None)
     p.add_argument("--precision", choices=["f64", "f32"], default=None)
+    p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                   help="strong (default): the configured lattice over N ranks; weak: N times the "
+                        "configured width (K4 weak scaling: (nx*N) x ny, one configured lattice per rank)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU sample duration")
     p.add_argument("--no-profile-events", action="store_true", help="skip per-launch HIP events")
@@ -160,6 +165,8 @@ def main():
 
     wnx, wny, wprec, wpts, wdesc = WORKLOADS[a.workload]
     nx, ny = a.nx or wnx, a.ny or wny
+    if a.scaling == "weak":
+        nx *= world
     precision = a.precision or wprec
     points = workload_points(wpts, nx)
     ns = 0 if points is None else points[0].size // 2
@@ -262,7 +269,7 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 5),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": precision,
             "data": "synthetic (rho = 1 + 1e-3 xi, u = 1e-3 xi, numpy seed 12345; body force 1e-6)",
