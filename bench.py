@@ -188,11 +188,12 @@ def main():
 
     lat.step(a.warmup)
     lat.synchronize()
-    # Launch timing for the roofline: HIP events around every collide launch.  At N = 1 they
-    # bracket the launches of the timed region itself (cost < 0.1 % at 4096^2).  At N > 1 a
-    # slab step is ~60 us and two event records per launch add several us, so the timed region
-    # runs without them and the same number of steps (<= 100) is timed with events afterwards.
-    events_in_timed = not distributed and not a.no_profile_events
+    # Launch timing for the roofline: HIP events around every collide launch.  At N = 1 without
+    # IB they bracket the launches of the timed region itself (one sweep launch per two steps:
+    # ~1 % at 4096^2, profiles/r01x_*).  At N > 1 (a slab cycle is ~70 us) and with IB (two
+    # launches per step: +4 event records, 4-8 % of the step) the timed region runs without them
+    # and the same number of steps (<= 100) is timed with events right afterwards.
+    events_in_timed = not distributed and not a.no_profile_events and ns == 0
     lat.set_profiling(events_in_timed)
     lat.timing(reset=True)
 
@@ -208,7 +209,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     tm = lat.timing(reset=True)
-    if distributed and not a.no_profile_events:
+    if not events_in_timed and not a.no_profile_events:
         lat.set_profiling(True)
         lat.step(min(a.steps, 100))
         lat.synchronize()
@@ -299,6 +300,8 @@ def main():
                 "cells_per_launch": cells_per_launch,
                 "iterations_per_launch": iters_per_launch,
                 "launch_ms": round(launch_ms, 5),
+                "launch_timing": ("HIP events in the timed region" if events_in_timed else
+                                  f"HIP events over {min(a.steps, 100)} further steps after the timed region"),
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,

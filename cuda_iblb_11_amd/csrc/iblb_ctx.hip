@@ -204,9 +204,12 @@ void ev_account(iblb_ctx* c, const iblb_ctx::EvRec& r, float ms) {
 int ev_begin(iblb_ctx* c, size_t* idx, hipStream_t st = nullptr) {
     if (!c->prof) return IBLB_OK;
     if (c->ev_used + 2 > c->ev_pool.size()) {
+        // timing events bracket kernels of this device only: no system-scope fence
+        // (IBLB_PROF_EVENT_FENCE=0 restores HIP's default release / acquire at system scope)
+        const unsigned flags = env_long("IBLB_PROF_EVENT_FENCE", 1) ? hipEventDisableSystemFence : 0u;
         for (int k = 0; k < 64; ++k) {
             hipEvent_t e;
-            HIP_TRY(c, hipEventCreate(&e));
+            HIP_TRY(c, hipEventCreateWithFlags(&e, flags));
             c->ev_pool.push_back(e);
         }
     }
