@@ -389,6 +389,225 @@ hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
+// ---- three iterations per launch (lone slab) ---------------------------------------------------
+// sweep3_kernel: g^t -> g^{t+3}, the walk keeping two register windows (g^{t+1}, g^{t+2}).  Same
+// wave geometry, order and walking directions as sweep2_kernel.  Valid rows shrink by one per
+// level at the wave's edges (the +-1-row pulls of the end lanes take garbage from level 2 on):
+// with VS >= 2 rows per lane the ghost lanes 0 and 63 still hold every row the owned lanes pull,
+// so VS = 2 (f64) and VS = 4 or 2 (f32) carry three levels.  Each level's cell arithmetic is
+// fused_kernel's (relax_cell): bit-identical to three one-step launches.
+//
+// Software-pipelined walk over the level-1 columns xa-2 .. xb+1 (dx = +1, or -1 from xb+1 down):
+// iteration i issues the loads of g^t column x, computes level 2 of column x-2dx and level 3 of
+// column x-3dx (which need nothing from those loads), then level 1 of column x.  The loads fly
+// while two levels of arithmetic run, without a second register set for a prefetched column.
+//
+// Algorithmic HBM bytes per launch: one read + one write of the state (144 B per cell in f64)
+// for THREE lattice updates, plus the edge re-reads of the neighbouring sweeps (served by L2 under
+// the XCD-contiguous alternating order).
+
+// plane k of column x of a lone slab, x periodic (x may lie up to 3 columns outside)
+template <typename T>
+__device__ __forceinline__ const T* col_periodic(const Sweep2Args<T>& a, int x, int k) {
+    const int n = a.L.ncol;
+    int xw = x % n;
+    if (xw < 0) xw += n;
+    return a.src + (long)xw * a.L.col + (long)k * a.L.plane;
+}
+
+template <typename T, int VS, int MODE>
+__device__ __forceinline__ void load_raw_periodic(const Sweep2Args<T>& a, int x, int row0, unsigned off, bool bot,
+                                                  bool top, Raw<T, VS>& r) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const T* p = col_periodic<T>(a, x - cx(k), k) + row0;
+        ld_rows<T, VS, MODE>(p, off, r.v[k]);
+        if (cy(k) == 1) r.e[k] = p[-1];
+        if (cy(k) == -1) r.e[k] = p[64 * VS];
+    }
+    r.w[0] = r.w[1] = r.w[2] = r.w[3] = (T)0;
+    if (bot) {
+        r.w[0] = col_periodic<T>(a, x, 7)[0];
+        r.w[1] = col_periodic<T>(a, x, 8)[0];
+    }
+    if (top) {
+        r.w[2] = col_periodic<T>(a, x, 5)[a.L.ny - 1];
+        r.w[3] = col_periodic<T>(a, x, 6)[a.L.ny - 1];
+    }
+}
+
+// one column of level l+1 from a window of level l (A = older, B = middle, C = newer column in
+// walking direction DX): the output is B's column; flux: add u_x of the owned rows to q
+template <typename T, int VS, int DX>
+__device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (&B)[9][VS], const T (&C)[9][VS],
+                                                  const Sweep2Args<T>& a, int lane, int r0, int et, bool flux,
+                                                  bool owner, double& q, T (&out)[9][VS]) {
+    typedef typename Calc<T>::R R;
+    constexpr bool DEV = Store<T>::dev;
+    const T(*pk[9])[VS];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) pk[k] = cx(k) == DX ? &A[k] : (cx(k) == -DX ? &C[k] : &B[k]);
+    T s[9][VS];
+    pull_window<T, VS>(pk, nullptr, B[2], B[4], B[7][0], B[8][0], B[5], B[6], lane, r0, et, s);
+#pragma unroll
+    for (int e = 0; e < VS; ++e) {
+        R f[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
+        const R ux = relax_cell<R, DEV>(f, a.c.gx, a.c.gy, a.c);
+        if (flux && owner && r0 + e < a.L.ny) q += (double)ux / a.flux_norm;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) out[k][e] = (T)f[k];
+    }
+}
+
+template <typename T, int VS>
+__device__ __forceinline__ void copy_col(T (&d)[9][VS], const T (&s)[9][VS]) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int e = 0; e < VS; ++e) d[k][e] = s[k][e];
+}
+
+template <typename T, int VS, int MODE, bool REV>
+__device__ __forceinline__ double sweep3_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
+                                              int lane, int r0, int et, bool owner, bool bot, bool top) {
+    typedef typename Calc<T>::R R;
+    constexpr bool DEV = Store<T>::dev;
+    constexpr int DX = REV ? -1 : 1;
+    const Layout L = a.L;
+    const int x0 = REV ? xb + 1 : xa - 2;
+    const int nl1 = xb - xa + 4;  // level-1 columns xa-2 .. xb+1
+    // level-1 window A1 = g1[x-3dx], B1 = g1[x-2dx], C1 = g1[x-dx]; level 2: A2 = g2[x-4dx], B2 = g2[x-3dx]
+    T A1[9][VS], B1[9][VS], C1[9][VS], A2[9][VS], B2[9][VS];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int e = 0; e < VS; ++e) { A1[k][e] = B1[k][e] = C1[k][e] = A2[k][e] = B2[k][e] = (T)0; }
+    double q = 0.;
+    for (int i = 0; i <= nl1; ++i) {
+        const int x = x0 + i * DX;
+        const bool l1 = i < nl1;
+        Raw<T, VS> cur;
+        if (l1) load_raw_periodic<T, VS, MODE>(a, x, row0, off, bot, top, cur);
+
+        // ---- level 2 of column x-2dx ----
+        T N2[9][VS];
+        if (i >= 3) {
+            const int c2 = x - 2 * DX;
+            level_from_window<T, VS, DX>(A1, B1, C1, a, lane, r0, et, c2 == a.flux_col && c2 >= xa && c2 < xb, owner,
+                                         q, N2);
+        }
+        // ---- level 3 of column x-3dx: the output ----
+        if (i >= 5) {
+            const int xo = x - 3 * DX;
+            T O[9][VS];
+            level_from_window<T, VS, DX>(A2, B2, N2, a, lane, r0, et, xo == a.flux_col, owner, q, O);
+            if (owner) {
+                T* dst = a.dst + (long)xo * L.col + row0;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * L.plane, off, O[k]);
+            }
+        }
+        // ---- level 1 of column x from the loads ----
+        T N1[9][VS];
+        if (l1) {
+            const T(*pk[9])[VS];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) pk[k] = &cur.v[k];
+            T s[9][VS];
+            T t5[VS], t6[VS];
+#pragma unroll
+            for (int e = 0; e < VS; ++e) { t5[e] = cur.w[2]; t6[e] = cur.w[3]; }
+            pull_window<T, VS>(pk, cur.e, cur.v[2], cur.v[4], cur.w[0], cur.w[1], t5, t6, lane, r0, et, s);
+            const bool flux1 = x == a.flux_col && x >= xa && x < xb;
+#pragma unroll
+            for (int e = 0; e < VS; ++e) {
+                R f[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
+                const R ux = relax_cell<R, DEV>(f, a.c.gx, a.c.gy, a.c);
+                if (flux1 && owner && r0 + e < L.ny) q += (double)ux / a.flux_norm;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) N1[k][e] = (T)f[k];
+            }
+        }
+        // ---- rotate the windows ----
+        if (i >= 3) {
+            copy_col<T, VS>(A2, B2);
+            copy_col<T, VS>(B2, N2);
+        }
+        copy_col<T, VS>(A1, B1);
+        copy_col<T, VS>(B1, C1);
+        if (l1) copy_col<T, VS>(C1, N1);
+    }
+    return q;
+}
+
+// wave -> (sweep, chunk) of the linear order, optionally dealt to the XCDs in contiguous ranges
+__device__ __forceinline__ void linear_item(int map, int nch, int wv, int& sw, int& ch) {
+    int b = (int)blockIdx.x;
+    if (map == 2) {
+        const int q = (int)gridDim.x / 8;
+        if (b < 8 * q) b = (b % 8) * q + b / 8;
+    }
+    const int gw = b * 4 + wv;
+    sw = gw / nch;
+    ch = gw - sw * nch;
+}
+
+template <typename T, int VS, int MODE>
+__global__ __launch_bounds__(256) void sweep3_kernel(Sweep2Args<T> a) {
+    static_assert(VS >= 2, "three levels need two ghost rows per wave edge (VS >= 2)");
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int sw, ch;
+    linear_item(a.map, a.nch, wv, sw, ch);
+    if (sw >= a.nsweep || ch >= a.nch) return;
+    const int xa = a.col_begin + sw * a.col_step;
+    const int xb = min(xa + a.W, a.col_end);
+    const int cs = ch * (62 * VS);
+    const int row0 = cs - VS;
+    const int r0 = row0 + lane * VS;
+    const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
+    const int et = a.L.ny - 1 - r0;
+    const bool owner = lane >= 1 && lane <= 62 && r0 < a.L.ny;
+    const bool bot = r0 == 0;
+    const bool top = et >= 0 && et < VS;
+    const double q = (a.alt && (sw & 1))
+                         ? sweep3_walk<T, VS, MODE, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
+                         : sweep3_walk<T, VS, MODE, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top);
+    if (a.flux_col >= xa && a.flux_col < xb) {
+        const double qs = wave_sum(q);
+        if (lane == 0) atomicAdd(a.Q, qs);
+    }
+}
+
+template <typename T, int VS>
+static hipError_t launch_sweep3_vs(const Sweep2Args<T>& a, unsigned blocks, hipStream_t s) {
+    switch (a.variant) {
+        case 0: sweep3_kernel<T, VS, 0><<<blocks, 256, 0, s>>>(a); break;
+        case 3: sweep3_kernel<T, VS, 3><<<blocks, 256, 0, s>>>(a); break;
+        default: sweep3_kernel<T, VS, 1><<<blocks, 256, 0, s>>>(a); break;
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_sweep3(Sweep2Args<T> a, hipStream_t s) {
+    if (a.nsweep <= 0) return hipSuccess;
+    // rows are read from row0 - 1 >= -VS - 1 to nch*62*VS + VS: inside the 512-element guards
+    if (a.W <= 0 || a.L.ncol < 1 || a.vs <= 0 || a.map == 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 ||
+        a.L.col % a.vs != 0)
+        return hipErrorInvalidValue;
+    a.nch = (a.L.ny + 62 * a.vs - 1) / (62 * a.vs);
+    const unsigned blocks = (unsigned)(((long)a.nsweep * a.nch + 3) / 4);
+    constexpr int V = vec_of<T>();
+    if (a.vs == V && V >= 2) return launch_sweep3_vs<T, (V >= 2 ? V : 2)>(a, blocks, s);
+    if (sizeof(T) == 4 && a.vs == 2) return launch_sweep3_vs<T, 2>(a, blocks, s);
+    return hipErrorInvalidValue;
+}
+
 // 2-step halo of g into the send buffers (slot layout in iblb_kernels.h); one thread per
 // (side, slot, row)
 template <typename T>
@@ -425,5 +644,7 @@ template hipError_t launch_pack_sweep_halo<double>(const double*, Layout, double
 template hipError_t launch_pack_sweep_halo<float>(const float*, Layout, float*, float*, hipStream_t);
 template hipError_t launch_sweep2<double>(Sweep2Args<double>, bool, hipStream_t);
 template hipError_t launch_sweep2<float>(Sweep2Args<float>, bool, hipStream_t);
+template hipError_t launch_sweep3<double>(Sweep2Args<double>, hipStream_t);
+template hipError_t launch_sweep3<float>(Sweep2Args<float>, hipStream_t);
 
 }  // namespace iblb

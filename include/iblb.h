@@ -140,6 +140,11 @@ typedef struct iblb_timing {
     long long sweep_launches;  /* timed two-iteration launches                           */
     double    sweep_ms;        /* their summed duration                                  */
     long long sweep_cells;     /* cells they covered (lattice updates = 2 x sweep_cells) */
+    /* three-iteration launches (lone slab, IBLB_SWEEP_DEPTH=3): state read and written once
+     * for three iterations */
+    long long sweep3_launches;
+    double    sweep3_ms;
+    long long sweep3_cells;    /* lattice updates = 3 x sweep3_cells */
 } iblb_timing;
 
 /* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */

@@ -1,0 +1,28 @@
+#!/bin/bash
+# Three iterations per launch (IBLB_SWEEP_DEPTH=3): bit identity, then step time against the
+# two-iteration default over sweep lengths, variants and cells per lane.
+set -eo pipefail
+export TMPDIR=/tmp
+T=${ROUND_TAG:-r01z}
+OUT=gpurun_out/$T
+mkdir -p "$OUT"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_fused.py -m gpu -x -q -p no:cacheprovider --timeout 250 \
+  --timeout-method thread -k "three_iterations" > "$OUT/pytest_sweep3.log" 2>&1 || { tail -30 "$OUT/pytest_sweep3.log"; exit 1; }
+tail -1 "$OUT/pytest_sweep3.log"
+fmt() { grep config "$1" | python -c "
+import sys,json
+for l in sys.stdin:
+    d=json.loads(l); print(f\"{d['config']:62s} {d['median_ms_per_iter']:.4f} ms/it {d['mlups']:9.0f} MLUPS same={d['bitwise_equal_to_first']}\")"; }
+E="IBLB_SWEEP_DEPTH=2"
+for w in 4 6 8 12; do for v in 1 3 0; do E="$E;IBLB_SWEEP_DEPTH=3 IBLB_SWEEP3_W=$w IBLB_SWEEP3_VARIANT=$v"; done; done
+echo "-- f64 4096^2"
+timeout -k 10 400 python -u scripts/tune_fused.py --steps 96 --rounds 3 --envs "$E" > "$OUT/tune_f64.log" 2>&1 \
+  || { tail -20 "$OUT/tune_f64.log"; exit 1; }
+fmt "$OUT/tune_f64.log"
+E="IBLB_SWEEP_DEPTH=2"
+for w in 4 6 8; do for vs in 4 2; do E="$E;IBLB_SWEEP_DEPTH=3 IBLB_SWEEP3_W=$w IBLB_SWEEP3_VS=$vs"; done; done
+echo "-- f32 4096^2"
+timeout -k 10 300 python -u scripts/tune_fused.py --precision f32 --steps 96 --rounds 3 --envs "$E" > "$OUT/tune_f32.log" 2>&1 \
+  || { tail -20 "$OUT/tune_f32.log"; exit 1; }
+fmt "$OUT/tune_f32.log"
+echo "== done"

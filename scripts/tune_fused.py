@@ -52,7 +52,8 @@ def main():
             sets.append((grp, e))
     names = sorted({k for _, e in sets for k in e} | {"IBLB_FUSED_VARIANT", "IBLB_PLANE_PAD", "IBLB_BUF_GAP",
                                                      "IBLB_SWEEP", "IBLB_SWEEP_W", "IBLB_SWEEP_VS", "IBLB_SWEEP_VARIANT",
-                                                     "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT"})
+                                                     "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT", "IBLB_SWEEP_DEPTH",
+                                                     "IBLB_SWEEP3_W", "IBLB_SWEEP3_VS", "IBLB_SWEEP3_VARIANT"})
     ctxs = []
     for key, e in sets:
         for name in names:
@@ -72,7 +73,8 @@ def main():
             lat.step(a.steps)
             t = lat.timing(reset=True)
             # time per iteration: one-step launches count once, two-iteration sweeps twice
-            res[k].append((t["fused_ms"] + t["sweep_ms"]) / (t["fused_launches"] + 2 * t["sweep_launches"]))
+            res[k].append((t["fused_ms"] + t["sweep_ms"] + t["sweep3_ms"]) /
+                          (t["fused_launches"] + 2 * t["sweep_launches"] + 3 * t["sweep3_launches"]))
         print(f"round {r} done", flush=True)
     bpc = 18 * (8 if a.precision == "f64" else 4)
     cells = a.nx * a.ny
