@@ -240,12 +240,12 @@ def main():
             launch_ms = float(sl.item())
         cells_per_launch = tm["sweep_cells"] // tm["sweep_launches"]
         iters_per_launch = 2
-    # three iterations per launch (lone slab, IBLB_SWEEP_DEPTH=3)
-    if tm["sweep3_launches"] > 0 and tm["sweep3_launches"] >= max(tm["sweep_launches"], tm["fused_launches"]):
-        sweep = 3
-        launch_ms = tm["sweep3_ms"] / tm["sweep3_launches"]
-        cells_per_launch = tm["sweep3_cells"] // tm["sweep3_launches"]
-        iters_per_launch = 3
+    # K >= 3 iterations per launch (lone slab, IBLB_SWEEP_DEPTH=K)
+    if tm["sweepk_launches"] > 0 and tm["sweepk_launches"] >= max(tm["sweep_launches"], tm["fused_launches"]):
+        sweep = int(tm["sweepk_depth"])
+        launch_ms = tm["sweepk_ms"] / tm["sweepk_launches"]
+        cells_per_launch = tm["sweepk_cells"] // tm["sweepk_launches"]
+        iters_per_launch = sweep
 
     # sanity: the state must stay finite (macro() is collective for an RCCL group)
     rho_s, _ = lat.macro()
@@ -259,7 +259,7 @@ def main():
     mlups = cells * a.steps / elapsed / 1e6
     bytes_per_cell = 18 * (8 if precision == "f64" else 4)
     achieved = bytes_per_cell * cells_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else None
-    key = f"{precision}_{nx}x{ny}_n{world}" + (f"_ib{ns}" if ns else "") + ("_sweep3" if sweep == 3 else ("_sweep" if sweep else ""))
+    key = f"{precision}_{nx}x{ny}_n{world}" + (f"_ib{ns}" if ns else "") + (f"_sweep{sweep}" if sweep not in (False, True) else ("_sweep" if sweep else ""))
     traffic, traffic_src = pmc_traffic(key)
 
     if rank == 0:
@@ -283,10 +283,9 @@ def main():
             "config": {
                 "workload": f"{wdesc} ({nx}x{ny}): D2Q9 channel (periodic x, bounce-back y=0, mirror y=Y-1), "
                             f"TRT+Guo, reference TAU/TAU2; "
-                            + ({3: "three iterations per launch (pull-stream+collide three times, intermediate states "
-                                   "in registers)",
-                                True: "two iterations per launch (pull-stream+collide twice, intermediate state in "
-                                      "registers)"}.get(sweep, "one fused pull-stream+collide launch per step"))
+                            + (f"{iters_per_launch} iterations per launch (pull-stream+collide {iters_per_launch} times, "
+                               "intermediate states in registers)" if sweep else
+                               "one fused pull-stream+collide launch per step")
                             + (f"; IB: {ns} static Lagrangian points, interpolate+spread every step" if ns else ""),
                 "nx": nx, "ny": ny, "global_cells": cells, "ib_points": ns,
                 "parallelism": f"x-slab x{world}" + (" (RCCL halo)" if world > 1 else "")
@@ -302,9 +301,10 @@ def main():
                 "unit": "GB/s",
                 "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": {3: "sweep3_kernel (lbm_sweep.hip): three iterations per launch, state read and written once",
-                           True: "sweep2_kernel (lbm_sweep.hip): two iterations per launch, state read and written once",
-                           }.get(sweep, "fused_kernel (lbm_kernels.hip)"),
+                "kernel": (f"sweepk_kernel<K={iters_per_launch}> (lbm_sweep.hip): {iters_per_launch} iterations per "
+                           "launch, state read and written once" if iters_per_launch > 2 else
+                           "sweep2_kernel (lbm_sweep.hip): two iterations per launch, state read and written once"
+                           if sweep else "fused_kernel (lbm_kernels.hip)"),
                 "bytes_per_cell": bytes_per_cell,
                 "cells_per_launch": cells_per_launch,
                 "iterations_per_launch": iters_per_launch,

@@ -62,7 +62,7 @@ class Timing(C.Structure):
         ("fused_ms", C.c_double), ("ib_ms", C.c_double), ("halo_ms", C.c_double),
         ("fused_bytes", C.c_double), ("cells", C.c_longlong), ("fused_cells", C.c_longlong),
         ("sweep_launches", C.c_longlong), ("sweep_ms", C.c_double), ("sweep_cells", C.c_longlong),
-        ("sweep3_launches", C.c_longlong), ("sweep3_ms", C.c_double), ("sweep3_cells", C.c_longlong),
+        ("sweepk_launches", C.c_longlong), ("sweepk_ms", C.c_double), ("sweepk_cells", C.c_longlong), ("sweepk_depth", C.c_longlong),
     ]
 
 

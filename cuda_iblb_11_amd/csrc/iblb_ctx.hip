@@ -63,8 +63,8 @@ struct iblb_ctx {
     // IBLB_SWEEP (on), IBLB_SWEEP_W columns per wave, IBLB_SWEEP_VS cells per lane, variant
     bool sweep_on = true;
     int sweep_w = 4, sweep_vs = 2, sweep_variant = 1, sweep_map = 2, sweep_alt = 1;
-    // three iterations per launch on a lone slab (IBLB_SWEEP_DEPTH=3): columns per wave, cells per lane
-    int sweep_depth = 2, sweep3_w = 4, sweep3_vs = 2, sweep3_variant = 1;
+    // K = 3 or 4 iterations per launch on a lone slab (IBLB_SWEEP_DEPTH): columns per wave, cells per lane
+    int sweep_depth = 2, deep_w = 4, deep_vs = 2, deep_variant = 1, deep_balance = 1;
     hipStream_t stream = nullptr;
     Coef coef{};
     // populations: two buffers in one allocation (deterministic relative placement of the
@@ -125,9 +125,9 @@ struct iblb_ctx {
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
-    double fused_ms = 0., ib_ms = 0., halo_ms = 0., sweep_ms = 0., sweep3_ms = 0.;
-    long long fused_launches = 0, fused_cells = 0, sweep_launches = 0, sweep_cells = 0, sweep3_launches = 0,
-              sweep3_cells = 0;
+    double fused_ms = 0., ib_ms = 0., halo_ms = 0., sweep_ms = 0., sweepk_ms = 0.;
+    long long fused_launches = 0, fused_cells = 0, sweep_launches = 0, sweep_cells = 0, sweepk_launches = 0,
+              sweepk_cells = 0;
     struct EvRec { int kind; size_t idx; long long cells; };
     std::vector<EvRec> ev_kind;
     std::string err;
@@ -195,12 +195,12 @@ void send_ptrs(iblb_ctx* c, T* sl[3], T* sr[3]) {
 }
 
 // ---- profiling --------------------------------------------------------------------------
-enum EvKind { EV_FUSED = 0, EV_IB = 1, EV_HALO = 2, EV_SWEEP = 3, EV_SWEEP3 = 4 };
+enum EvKind { EV_FUSED = 0, EV_IB = 1, EV_HALO = 2, EV_SWEEP = 3, EV_SWEEPK = 4 };
 
 void ev_account(iblb_ctx* c, const iblb_ctx::EvRec& r, float ms) {
     if (r.kind == EV_FUSED) { c->fused_ms += ms; c->fused_launches++; c->fused_cells += r.cells; }
     else if (r.kind == EV_SWEEP) { c->sweep_ms += ms; c->sweep_launches++; c->sweep_cells += r.cells; }
-    else if (r.kind == EV_SWEEP3) { c->sweep3_ms += ms; c->sweep3_launches++; c->sweep3_cells += r.cells; }
+    else if (r.kind == EV_SWEEPK) { c->sweepk_ms += ms; c->sweepk_launches++; c->sweepk_cells += r.cells; }
     else if (r.kind == EV_IB) c->ib_ms += ms;
     else c->halo_ms += ms;
 }
@@ -499,21 +499,22 @@ void after_sweep(iblb_ctx* c) {
     c->halo_valid = false;
 }
 
-// three iterations in one launch (lone slab only; slabs of a group keep the 2-step halo)
+// K = sweep_depth iterations in one launch (lone slab only; slabs of a group keep the 2-step halo)
 template <typename T>
-int sweep3_step(iblb_ctx* c) {
-    const int W = std::max(1, c->sweep3_w);
-    Sweep2Args<T> a = sweep_args<T>(c, 0, W, c->ncol, (c->ncol + W - 1) / W, W);
-    a.vs = c->sweep3_vs;
-    a.variant = c->sweep3_variant;
+int sweepk_step(iblb_ctx* c) {
+    const int W = std::max(1, c->deep_w);
+    // balanced sweep widths (col_step 0: the launcher sizes the sweeps to whole rounds of waves)
+    Sweep2Args<T> a = sweep_args<T>(c, 0, c->deep_balance ? 0 : W, c->ncol, (c->ncol + W - 1) / W, W);
+    a.vs = c->deep_vs;
+    a.variant = c->deep_variant;
     if (a.map == 0) a.map = 2;
     size_t ev = 0;
     int rc = ev_begin(c, &ev, c->stream);
     if (rc) return rc;
-    HIP_TRY(c, launch_sweep3<T>(a, c->stream));
-    if ((rc = ev_end(c, ev, EV_SWEEP3, (long long)c->ncol * c->ny, c->stream))) return rc;
+    HIP_TRY(c, launch_sweepk<T>(a, c->sweep_depth, c->stream));
+    if ((rc = ev_end(c, ev, EV_SWEEPK, (long long)c->ncol * c->ny, c->stream))) return rc;
     c->cur = 1 - c->cur;
-    c->t += 3;
+    c->t += c->sweep_depth;
     c->halo_valid = false;
     return IBLB_OK;
 }
@@ -777,9 +778,11 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->sweep_map = (int)env_long("IBLB_SWEEP_MAP", 2);
     c->sweep_alt = (int)env_long("IBLB_SWEEP_ALT", 1);
     c->sweep_depth = (int)env_long("IBLB_SWEEP_DEPTH", 2);
-    c->sweep3_w = (int)env_long("IBLB_SWEEP3_W", 4);
-    c->sweep3_vs = (int)env_long("IBLB_SWEEP3_VS", c->prec == IBLB_PREC_F64 ? 2 : 4);
-    c->sweep3_variant = (int)env_long("IBLB_SWEEP3_VARIANT", 1);
+    if (c->sweep_depth > 4) c->sweep_depth = 4;
+    c->deep_w = (int)env_long("IBLB_DEEP_W", 4);
+    c->deep_vs = (int)env_long("IBLB_DEEP_VS", c->prec == IBLB_PREC_F64 ? 2 : 4);
+    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", 1);
+    c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     if (c->cfg.flux_column < 0) c->cfg.flux_column = c->nx - 5;
 
     const double tau = cfg->tau, tau2 = cfg->tau2, cs = 0.57735;
@@ -1040,9 +1043,9 @@ int iblb_step(iblb_ctx* c, int nsteps) {
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
     for (int s = 0; s < nsteps;) {
-        if (nsteps - s >= 3 && c->sweep_depth == 3 && single_slab(c) && sweep_ready(c)) {
-            if ((rc = c->prec == IBLB_PREC_F64 ? sweep3_step<double>(c) : sweep3_step<float>(c))) return rc;
-            s += 3;
+        if (c->sweep_depth >= 3 && nsteps - s >= c->sweep_depth && single_slab(c) && sweep_ready(c)) {
+            if ((rc = c->prec == IBLB_PREC_F64 ? sweepk_step<double>(c) : sweepk_step<float>(c))) return rc;
+            s += c->sweep_depth;
             continue;
         }
         if (nsteps - s >= 2 && sweep_ready(c)) {
@@ -1186,13 +1189,14 @@ int iblb_get_timing(iblb_ctx* c, iblb_timing* t, int reset) {
     t->sweep_launches = c->sweep_launches;
     t->sweep_ms = c->sweep_ms;
     t->sweep_cells = c->sweep_cells;
-    t->sweep3_launches = c->sweep3_launches;
-    t->sweep3_ms = c->sweep3_ms;
-    t->sweep3_cells = c->sweep3_cells;
+    t->sweepk_launches = c->sweepk_launches;
+    t->sweepk_ms = c->sweepk_ms;
+    t->sweepk_cells = c->sweepk_cells;
+    t->sweepk_depth = c->sweep_depth;
     if (reset) {
-        c->fused_ms = c->ib_ms = c->halo_ms = c->sweep_ms = c->sweep3_ms = 0.;
+        c->fused_ms = c->ib_ms = c->halo_ms = c->sweep_ms = c->sweepk_ms = 0.;
         c->fused_launches = c->fused_cells = c->sweep_launches = c->sweep_cells = 0;
-        c->sweep3_launches = c->sweep3_cells = 0;
+        c->sweepk_launches = c->sweepk_cells = 0;
     }
     return IBLB_OK;
 }

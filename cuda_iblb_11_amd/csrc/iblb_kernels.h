@@ -85,9 +85,10 @@ struct Sweep2Args {
 // slab (periodic images) or interior columns of a group slab (no halo, no sends)
 template <typename T>
 hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s);
-// Three iterations per launch on a lone slab (periodic columns): g^t -> g^{t+3}; map 1 or 2.
+// K = depth (3 or 4) iterations per launch on a lone slab (periodic columns): g^t -> g^{t+K};
+// map 1 or 2.
 template <typename T>
-hipError_t launch_sweep3(Sweep2Args<T> a, hipStream_t s);
+hipError_t launch_sweepk(Sweep2Args<T> a, int depth, hipStream_t s);
 // The 2-step halo of state g into both send buffers (after a one-step launch or an IB exchange).
 template <typename T>
 hipError_t launch_pack_sweep_halo(const T* g, Layout L, T* send_left, T* send_right, hipStream_t st);

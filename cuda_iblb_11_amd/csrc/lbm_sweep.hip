@@ -389,24 +389,24 @@ hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
-// ---- three iterations per launch (lone slab) ---------------------------------------------------
-// sweep3_kernel: g^t -> g^{t+3}, the walk keeping two register windows (g^{t+1}, g^{t+2}).  Same
-// wave geometry, order and walking directions as sweep2_kernel.  Valid rows shrink by one per
-// level at the wave's edges (the +-1-row pulls of the end lanes take garbage from level 2 on):
-// with VS >= 2 rows per lane the ghost lanes 0 and 63 still hold every row the owned lanes pull,
-// so VS = 2 (f64) and VS = 4 or 2 (f32) carry three levels.  Each level's cell arithmetic is
-// fused_kernel's (relax_cell): bit-identical to three one-step launches.
+// ---- K iterations per launch (lone slab, K = 3 or 4) ------------------------------------------
+// sweepk_kernel: g^t -> g^{t+K}, the walk keeping K-1 register windows (g^{t+1} .. g^{t+K-1}).
+// Same wave geometry, order and walking directions as sweep2_kernel.  Valid rows shrink by one
+// per level at the wave's edges (the +-1-row pulls of the end lanes take garbage from level 2
+// on), so each edge carries G ghost lanes with G * VS >= K - 1 rows.  Each level's cell
+// arithmetic is fused_kernel's (relax_cell): bit-identical to K one-step launches.
 //
-// Software-pipelined walk over the level-1 columns xa-2 .. xb+1 (dx = +1, or -1 from xb+1 down):
-// iteration i issues the loads of g^t column x, computes level 2 of column x-2dx and level 3 of
-// column x-3dx (which need nothing from those loads), then level 1 of column x.  The loads fly
-// while two levels of arithmetic run, without a second register set for a prefetched column.
+// Software-pipelined walk over the level-1 columns xa-(K-1) .. xb+(K-2) (dx = +1, or -1 from
+// the right end): iteration i issues the loads of g^t column x, computes level l >= 2 of column
+// x - l*dx (level 2 from level-1 columns of earlier iterations, level l > 2 from level l-1's
+// window and the column level l-1 made in this iteration), then level 1 of column x.  The loads
+// fly while K-1 levels of arithmetic run, without a second register set for a prefetched column.
 //
 // Algorithmic HBM bytes per launch: one read + one write of the state (144 B per cell in f64)
-// for THREE lattice updates, plus the edge re-reads of the neighbouring sweeps (served by L2 under
-// the XCD-contiguous alternating order).
+// for K lattice updates, plus the edge re-reads of neighbouring sweeps (served by L2 under the
+// XCD-contiguous alternating order).
 
-// plane k of column x of a lone slab, x periodic (x may lie up to 3 columns outside)
+// plane k of column x of a lone slab, x periodic (x may lie up to K columns outside)
 template <typename T>
 __device__ __forceinline__ const T* col_periodic(const Sweep2Args<T>& a, int x, int k) {
     const int n = a.L.ncol;
@@ -469,21 +469,27 @@ __device__ __forceinline__ void copy_col(T (&d)[9][VS], const T (&s)[9][VS]) {
         for (int e = 0; e < VS; ++e) d[k][e] = s[k][e];
 }
 
-template <typename T, int VS, int MODE, bool REV>
-__device__ __forceinline__ double sweep3_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
+template <typename T, int VS, int MODE, int K, bool REV>
+__device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
                                               int lane, int r0, int et, bool owner, bool bot, bool top) {
     typedef typename Calc<T>::R R;
     constexpr bool DEV = Store<T>::dev;
     constexpr int DX = REV ? -1 : 1;
     const Layout L = a.L;
-    const int x0 = REV ? xb + 1 : xa - 2;
-    const int nl1 = xb - xa + 4;  // level-1 columns xa-2 .. xb+1
-    // level-1 window A1 = g1[x-3dx], B1 = g1[x-2dx], C1 = g1[x-dx]; level 2: A2 = g2[x-4dx], B2 = g2[x-3dx]
-    T A1[9][VS], B1[9][VS], C1[9][VS], A2[9][VS], B2[9][VS];
+    const int x0 = REV ? xb + K - 2 : xa - (K - 1);
+    const int nl1 = xb - xa + 2 * (K - 1);  // level-1 columns xa-(K-1) .. xb+(K-2)
+    // level 1: A1 = g1[x-3dx], B1 = g1[x-2dx], C1 = g1[x-dx]; level l in 2..K-1: WA[l-2] and
+    // WB[l-2] = its columns x-(l+2)dx and x-(l+1)dx (the newest one is made in the iteration)
+    T A1[9][VS], B1[9][VS], C1[9][VS];
+    T WA[K - 2][9][VS], WB[K - 2][9][VS];
 #pragma unroll
     for (int k = 0; k < 9; ++k)
 #pragma unroll
-        for (int e = 0; e < VS; ++e) { A1[k][e] = B1[k][e] = C1[k][e] = A2[k][e] = B2[k][e] = (T)0; }
+        for (int e = 0; e < VS; ++e) {
+            A1[k][e] = B1[k][e] = C1[k][e] = (T)0;
+#pragma unroll
+            for (int l = 0; l < K - 2; ++l) WA[l][k][e] = WB[l][k][e] = (T)0;
+        }
     double q = 0.;
     for (int i = 0; i <= nl1; ++i) {
         const int x = x0 + i * DX;
@@ -491,23 +497,29 @@ __device__ __forceinline__ double sweep3_walk(const Sweep2Args<T>& a, int xa, in
         Raw<T, VS> cur;
         if (l1) load_raw_periodic<T, VS, MODE>(a, x, row0, off, bot, top, cur);
 
-        // ---- level 2 of column x-2dx ----
-        T N2[9][VS];
-        if (i >= 3) {
-            const int c2 = x - 2 * DX;
-            level_from_window<T, VS, DX>(A1, B1, C1, a, lane, r0, et, c2 == a.flux_col && c2 >= xa && c2 < xb, owner,
-                                         q, N2);
-        }
-        // ---- level 3 of column x-3dx: the output ----
-        if (i >= 5) {
-            const int xo = x - 3 * DX;
-            T O[9][VS];
-            level_from_window<T, VS, DX>(A2, B2, N2, a, lane, r0, et, xo == a.flux_col, owner, q, O);
-            if (owner) {
-                T* dst = a.dst + (long)xo * L.col + row0;
+        // ---- levels 2 .. K of columns x - l*dx ----
+        T N[9][VS];  // the column the previous level made in this iteration
 #pragma unroll
-                for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * L.plane, off, O[k]);
+        for (int l = 2; l <= K; ++l) {
+            T out[9][VS];
+            const bool made = i >= 2 * l - 1;
+            if (made) {
+                const int c = x - l * DX;
+                const bool flux = c == a.flux_col && c >= xa && c < xb;
+                if (l == 2) level_from_window<T, VS, DX>(A1, B1, C1, a, lane, r0, et, flux, owner, q, out);
+                else level_from_window<T, VS, DX>(WA[l - 3], WB[l - 3], N, a, lane, r0, et, flux, owner, q, out);
+                if (l == K && owner) {
+                    T* dst = a.dst + (long)c * L.col + row0;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * L.plane, off, out[k]);
+                }
             }
+            // level l-1 (>= 2) made N in this iteration: rotate its window
+            if (l >= 3 && i >= 2 * (l - 1) - 1) {
+                copy_col<T, VS>(WA[l - 3], WB[l - 3]);
+                copy_col<T, VS>(WB[l - 3], N);
+            }
+            if (made && l < K) copy_col<T, VS>(N, out);
         }
         // ---- level 1 of column x from the loads ----
         T N1[9][VS];
@@ -532,11 +544,6 @@ __device__ __forceinline__ double sweep3_walk(const Sweep2Args<T>& a, int xa, in
                 for (int k = 0; k < 9; ++k) N1[k][e] = (T)f[k];
             }
         }
-        // ---- rotate the windows ----
-        if (i >= 3) {
-            copy_col<T, VS>(A2, B2);
-            copy_col<T, VS>(B2, N2);
-        }
         copy_col<T, VS>(A1, B1);
         copy_col<T, VS>(B1, C1);
         if (l1) copy_col<T, VS>(C1, N1);
@@ -556,55 +563,112 @@ __device__ __forceinline__ void linear_item(int map, int nch, int wv, int& sw, i
     ch = gw - sw * nch;
 }
 
-template <typename T, int VS, int MODE>
-__global__ __launch_bounds__(256) void sweep3_kernel(Sweep2Args<T> a) {
-    static_assert(VS >= 2, "three levels need two ghost rows per wave edge (VS >= 2)");
+template <int K, int VS>
+constexpr int ghost_lanes() { return (K - 1 + VS - 1) / VS; }
+
+// G ghost lanes at each wave edge (G * VS >= K - 1 rows)
+template <typename T, int VS, int MODE, int K>
+__global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
+    constexpr int G = ghost_lanes<K, VS>();
+    constexpr int OWN = 64 - 2 * G;  // owned lanes per wave
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int sw, ch;
     linear_item(a.map, a.nch, wv, sw, ch);
     if (sw >= a.nsweep || ch >= a.nch) return;
-    const int xa = a.col_begin + sw * a.col_step;
-    const int xb = min(xa + a.W, a.col_end);
-    const int cs = ch * (62 * VS);
-    const int row0 = cs - VS;
+    int xa, xb;
+    if (a.col_step > 0) {
+        xa = a.col_begin + sw * a.col_step;
+        xb = min(xa + a.W, a.col_end);
+    } else {  // balanced: nsweep sweeps of floor/ceil((col_end - col_begin) / nsweep) columns
+        const long n = a.col_end - a.col_begin;
+        xa = a.col_begin + (int)(sw * n / a.nsweep);
+        xb = a.col_begin + (int)((sw + 1) * n / a.nsweep);
+    }
+    const int cs = ch * (OWN * VS);
+    const int row0 = cs - G * VS;
     const int r0 = row0 + lane * VS;
     const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
     const int et = a.L.ny - 1 - r0;
-    const bool owner = lane >= 1 && lane <= 62 && r0 < a.L.ny;
+    const bool owner = lane >= G && lane < 64 - G && r0 < a.L.ny;
     const bool bot = r0 == 0;
     const bool top = et >= 0 && et < VS;
     const double q = (a.alt && (sw & 1))
-                         ? sweep3_walk<T, VS, MODE, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
-                         : sweep3_walk<T, VS, MODE, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top);
+                         ? sweepk_walk<T, VS, MODE, K, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
+                         : sweepk_walk<T, VS, MODE, K, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top);
     if (a.flux_col >= xa && a.flux_col < xb) {
         const double qs = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, qs);
     }
 }
 
-template <typename T, int VS>
-static hipError_t launch_sweep3_vs(const Sweep2Args<T>& a, unsigned blocks, hipStream_t s) {
-    switch (a.variant) {
-        case 0: sweep3_kernel<T, VS, 0><<<blocks, 256, 0, s>>>(a); break;
-        case 3: sweep3_kernel<T, VS, 3><<<blocks, 256, 0, s>>>(a); break;
-        default: sweep3_kernel<T, VS, 1><<<blocks, 256, 0, s>>>(a); break;
+// Waves resident on the whole device for one instantiation (256-thread workgroups).
+template <typename T, int VS, int MODE, int K>
+static long resident_waves() {
+    static long cached = 0;
+    if (cached) return cached;
+    int dev = 0, ncu = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweepk_kernel<T, VS, MODE, K>, 256, 0) != hipSuccess ||
+        nb <= 0 || ncu <= 0)
+        return 0;
+    cached = (long)nb * 4 * ncu;
+    return cached;
+}
+
+template <typename T, int VS, int MODE, int K>
+static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s) {
+    if (b.col_step <= 0) {
+        // balanced sweeps: the wave count a whole number of device-wide rounds (the waves of one
+        // launch all do the same work, so a partial last round idles the chip), sweeps close to
+        // the requested W columns
+        const long n = b.col_end - b.col_begin;
+        const long slots = resident_waves<T, VS, MODE, K>();
+        long ns = (n + b.W - 1) / b.W;
+        if (slots > 0) {
+            const long rounds = std::max(1L, (ns * b.nch + slots / 2) / slots);
+            ns = std::max(1L, rounds * slots / b.nch);
+        }
+        b.nsweep = (int)std::min(ns, n);
     }
+    const unsigned blocks = (unsigned)(((long)b.nsweep * b.nch + 3) / 4);
+    sweepk_kernel<T, VS, MODE, K><<<blocks, 256, 0, s>>>(b);
     return hipGetLastError();
 }
 
+template <typename T, int VS, int K>
+static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s) {
+    constexpr int G = ghost_lanes<K, VS>();
+    const int rows_per_wave = (64 - 2 * G) * VS;  // owned rows
+    Sweep2Args<T> b = a;
+    b.nch = (a.L.ny + rows_per_wave - 1) / rows_per_wave;
+    switch (a.variant) {
+        case 0: return launch_sweepk_mode<T, VS, 0, K>(b, s);
+        case 3: return launch_sweepk_mode<T, VS, 3, K>(b, s);
+        default: return launch_sweepk_mode<T, VS, 1, K>(b, s);
+    }
+}
+
+template <typename T, int K>
+static hipError_t launch_sweepk_depth(const Sweep2Args<T>& a, hipStream_t s) {
+    constexpr int V = vec_of<T>();
+    if (a.vs == V) return launch_sweepk_vs<T, V, K>(a, s);
+    if (a.vs == V / 2) return launch_sweepk_vs<T, V / 2, K>(a, s);
+    if (V == 4 && a.vs == 1) return launch_sweepk_vs<T, 1, K>(a, s);
+    return hipErrorInvalidValue;
+}
+
 template <typename T>
-hipError_t launch_sweep3(Sweep2Args<T> a, hipStream_t s) {
+hipError_t launch_sweepk(Sweep2Args<T> a, int depth, hipStream_t s) {
     if (a.nsweep <= 0) return hipSuccess;
-    // rows are read from row0 - 1 >= -VS - 1 to nch*62*VS + VS: inside the 512-element guards
+    // rows are read from row0 - 1 >= -(K-1) - VS - 1 to the last wave's row0 + 64*VS: inside the
+    // 512-element guards of the buffers
     if (a.W <= 0 || a.L.ncol < 1 || a.vs <= 0 || a.map == 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 ||
         a.L.col % a.vs != 0)
         return hipErrorInvalidValue;
-    a.nch = (a.L.ny + 62 * a.vs - 1) / (62 * a.vs);
-    const unsigned blocks = (unsigned)(((long)a.nsweep * a.nch + 3) / 4);
-    constexpr int V = vec_of<T>();
-    if (a.vs == V && V >= 2) return launch_sweep3_vs<T, (V >= 2 ? V : 2)>(a, blocks, s);
-    if (sizeof(T) == 4 && a.vs == 2) return launch_sweep3_vs<T, 2>(a, blocks, s);
+    if (depth == 3) return launch_sweepk_depth<T, 3>(a, s);
+    if (depth == 4) return launch_sweepk_depth<T, 4>(a, s);
     return hipErrorInvalidValue;
 }
 
@@ -644,7 +708,7 @@ template hipError_t launch_pack_sweep_halo<double>(const double*, Layout, double
 template hipError_t launch_pack_sweep_halo<float>(const float*, Layout, float*, float*, hipStream_t);
 template hipError_t launch_sweep2<double>(Sweep2Args<double>, bool, hipStream_t);
 template hipError_t launch_sweep2<float>(Sweep2Args<float>, bool, hipStream_t);
-template hipError_t launch_sweep3<double>(Sweep2Args<double>, hipStream_t);
-template hipError_t launch_sweep3<float>(Sweep2Args<float>, hipStream_t);
+template hipError_t launch_sweepk<double>(Sweep2Args<double>, int, hipStream_t);
+template hipError_t launch_sweepk<float>(Sweep2Args<float>, int, hipStream_t);
 
 }  // namespace iblb

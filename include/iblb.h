@@ -140,11 +140,12 @@ typedef struct iblb_timing {
     long long sweep_launches;  /* timed two-iteration launches                           */
     double    sweep_ms;        /* their summed duration                                  */
     long long sweep_cells;     /* cells they covered (lattice updates = 2 x sweep_cells) */
-    /* three-iteration launches (lone slab, IBLB_SWEEP_DEPTH=3): state read and written once
-     * for three iterations */
-    long long sweep3_launches;
-    double    sweep3_ms;
-    long long sweep3_cells;    /* lattice updates = 3 x sweep3_cells */
+    /* deep launches (lone slab, IBLB_SWEEP_DEPTH = K >= 3): state read and written once for K
+     * iterations */
+    long long sweepk_launches;
+    double    sweepk_ms;
+    long long sweepk_cells;    /* lattice updates = sweepk_depth x sweepk_cells */
+    long long sweepk_depth;    /* K */
 } iblb_timing;
 
 /* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */

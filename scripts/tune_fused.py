@@ -53,7 +53,7 @@ def main():
     names = sorted({k for _, e in sets for k in e} | {"IBLB_FUSED_VARIANT", "IBLB_PLANE_PAD", "IBLB_BUF_GAP",
                                                      "IBLB_SWEEP", "IBLB_SWEEP_W", "IBLB_SWEEP_VS", "IBLB_SWEEP_VARIANT",
                                                      "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT", "IBLB_SWEEP_DEPTH",
-                                                     "IBLB_SWEEP3_W", "IBLB_SWEEP3_VS", "IBLB_SWEEP3_VARIANT"})
+                                                     "IBLB_DEEP_W", "IBLB_DEEP_VS", "IBLB_DEEP_VARIANT", "IBLB_DEEP_BALANCE"})
     ctxs = []
     for key, e in sets:
         for name in names:
@@ -73,8 +73,8 @@ def main():
             lat.step(a.steps)
             t = lat.timing(reset=True)
             # time per iteration: one-step launches count once, two-iteration sweeps twice
-            res[k].append((t["fused_ms"] + t["sweep_ms"] + t["sweep3_ms"]) /
-                          (t["fused_launches"] + 2 * t["sweep_launches"] + 3 * t["sweep3_launches"]))
+            res[k].append((t["fused_ms"] + t["sweep_ms"] + t["sweepk_ms"]) /
+                          (t["fused_launches"] + 2 * t["sweep_launches"] + t["sweepk_depth"] * t["sweepk_launches"]))
         print(f"round {r} done", flush=True)
     bpc = 18 * (8 if a.precision == "f64" else 4)
     cells = a.nx * a.ny

@@ -462,44 +462,50 @@ def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap):
     ring.close()
 
 
+@pytest.mark.parametrize("depth", [3, 4])
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-def test_sweep_three_iterations_bit_identical(gpu, oracle, precision, monkeypatch):
-    """Three iterations per launch (IBLB_SWEEP_DEPTH=3, lone slab: two register windows, the
-    chunk-edge ghost rows shrinking by one per level) equal one-step launches bit for bit, for
-    every sweep length, variant, wave order and walking direction, on ragged shapes including
-    fewer columns than the 3-column reach (periodic images wrap more than once).  33 steps =
-    boot + 10 three-iteration launches + one two-iteration launch."""
+def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
+    """K = 3 or 4 iterations per launch (IBLB_SWEEP_DEPTH=K, lone slab: K-1 register windows,
+    the chunk-edge ghost rows shrinking by one per level, ceil((K-1)/VS) ghost lanes per edge)
+    equal one-step launches bit for bit, for every cells-per-lane width, sweep length (fixed
+    and balanced to whole rounds of waves), variant, wave order and walking direction, on
+    ragged shapes including fewer columns than the K-column reach (periodic images wrap more
+    than once).  1 + 10K + 2 steps = boot + 10 deep launches + one two-iteration launch."""
     from cuda_iblb_11_amd import workloads as W
-    vss = [2] if precision == "f64" else [4, 2]
+    vss = [2, 1] if precision == "f64" else [4, 2, 1]
+    steps = 1 + 10 * depth + 2
     for nx, ny in [(37, 300), (2, 63), (5, 1100), (70, 125), (3, 130)]:
         rho, u = W.perturbed_state(nx, ny, 7)
         monkeypatch.setenv("IBLB_SWEEP", "0")
         ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 3e-7))
         ref.set_state(rho, u)
-        ref.step(33)
+        ref.step(steps)
         f_ref, q_ref = ref.populations(), ref.flux
         ref.close()
         monkeypatch.setenv("IBLB_SWEEP", "1")
-        monkeypatch.setenv("IBLB_SWEEP_DEPTH", "3")
+        monkeypatch.setenv("IBLB_SWEEP_DEPTH", str(depth))
         for vs in vss:
-            for w, var, mp, alt in [(4, 1, 2, 1), (1, 0, 1, 0), (3, 3, 2, 0), (32, 1, 1, 1), (7, 0, 2, 1)]:
-                monkeypatch.setenv("IBLB_SWEEP3_VS", str(vs))
-                monkeypatch.setenv("IBLB_SWEEP3_W", str(w))
-                monkeypatch.setenv("IBLB_SWEEP3_VARIANT", str(var))
+            for w, var, mp, alt, bal in [(4, 1, 2, 1, 0), (1, 0, 1, 0, 0), (3, 3, 2, 0, 1), (32, 1, 1, 1, 0),
+                                         (7, 0, 2, 1, 1), (48, 1, 2, 1, 1)]:
+                monkeypatch.setenv("IBLB_DEEP_VS", str(vs))
+                monkeypatch.setenv("IBLB_DEEP_W", str(w))
+                monkeypatch.setenv("IBLB_DEEP_VARIANT", str(var))
+                monkeypatch.setenv("IBLB_DEEP_BALANCE", str(bal))
                 monkeypatch.setenv("IBLB_SWEEP_MAP", str(mp))
                 monkeypatch.setenv("IBLB_SWEEP_ALT", str(alt))
                 lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 3e-7))
                 lat.set_state(rho, u)
                 lat.set_profiling(True)
-                lat.step(33)
+                lat.step(steps)
                 tm = lat.timing()
-                assert tm["sweep3_launches"] == 10 and tm["sweep_launches"] == 1, tm
+                assert tm["sweepk_launches"] == 10 and tm["sweep_launches"] == 1 and tm["sweepk_depth"] == depth, tm
                 f = lat.populations()
-                assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, mp, alt, float(np.max(np.abs(f - f_ref))))
+                assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, mp, alt, bal,
+                                                  float(np.max(np.abs(f - f_ref))))
                 assert abs(lat.flux - q_ref) <= 1e-12 * abs(q_ref), (lat.flux, q_ref)
                 lat.close()
-    for name in ("IBLB_SWEEP_DEPTH", "IBLB_SWEEP3_VS", "IBLB_SWEEP3_W", "IBLB_SWEEP3_VARIANT", "IBLB_SWEEP_MAP",
-                 "IBLB_SWEEP_ALT"):
+    for name in ("IBLB_SWEEP_DEPTH", "IBLB_DEEP_VS", "IBLB_DEEP_W", "IBLB_DEEP_VARIANT", "IBLB_DEEP_BALANCE",
+                 "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT"):
         monkeypatch.delenv(name)
 
 
