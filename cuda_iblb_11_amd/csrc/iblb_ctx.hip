@@ -63,7 +63,7 @@ struct iblb_ctx {
     // IBLB_SWEEP (on), IBLB_SWEEP_W columns per wave, IBLB_SWEEP_VS cells per lane, variant
     bool sweep_on = true;
     int sweep_w = 4, sweep_vs = 2, sweep_variant = 1, sweep_map = 2, sweep_alt = 1;
-    // K = 3 or 4 iterations per launch on a lone slab (IBLB_SWEEP_DEPTH): columns per wave, cells per lane
+    // K = 3 .. 6 iterations per launch on a lone slab (IBLB_SWEEP_DEPTH): columns per wave, cells per lane
     int sweep_depth = 2, deep_w = 4, deep_vs = 2, deep_variant = 1, deep_balance = 1;
     hipStream_t stream = nullptr;
     Coef coef{};
@@ -106,6 +106,7 @@ struct iblb_ctx {
     bool halo_valid = false;
     bool halo_ib = false;  // the received halo carries the IB slots (IB_HALO_SLOTS)
     bool send_sweep = false;  // the send buffers hold the 2-step halo of the current state
+    int send_deep = 0;        // ... or the deep halo of this depth (deep_slot layout), 0 = none
     int halo_slots = HALO_SLOTS;  // slots per halo buffer (IB_HALO_SLOTS when IB-capable)
     // transport
     int transport = TR_NONE;
@@ -255,13 +256,15 @@ int pack_ib_any(iblb_ctx* c, hipStream_t st) {
 
 // ib: also carry the IB slots (the owed force is evaluated from this halo); sweep: the 2-step
 // halo (the send buffers hold it: written by the boundary sweep or packed)
-int exchange_rccl(iblb_ctx* c, hipStream_t st, bool ib = false, bool sweep = false) {
+int exchange_rccl(iblb_ctx* c, hipStream_t st, bool ib = false, bool sweep = false, int nslots = 0) {
     size_t ev = 0;
     int rc;
     if (ib && (rc = pack_ib_any(c, st))) return rc;
     if (ib) c->send_sweep = false;  // slots 3.. now carry the IB halo
+    if (ib) c->send_deep = 0;
     if ((rc = ev_begin(c, &ev, st))) return rc;
-    const size_t n = (size_t)(ib ? IB_HALO_SLOTS : (sweep ? SWEEP_HALO_SLOTS : HALO_SLOTS)) * c->L.rows;
+    if (nslots <= 0) nslots = ib ? IB_HALO_SLOTS : (sweep ? SWEEP_HALO_SLOTS : HALO_SLOTS);
+    const size_t n = (size_t)nslots * c->L.rows;
     const ncclDataType_t dt = c->prec == IBLB_PREC_F64 ? ncclFloat64 : ncclFloat32;
     const int lr = (c->rank + c->nranks - 1) % c->nranks, rr = (c->rank + 1) % c->nranks;
     NCCL_TRY(c, ncclGroupStart());
@@ -300,6 +303,7 @@ int pack_send(iblb_ctx* c) {
                                   c->stream));
     }
     c->send_sweep = false;
+    c->send_deep = 0;
     if (rccl_multi(c)) {
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
@@ -411,6 +415,7 @@ int free_boot(iblb_ctx* c) {
 
 void after_step(iblb_ctx* c) {
     c->send_sweep = false;  // a one-step collide writes the one-step slots only
+    c->send_deep = 0;
     c->cur = 1 - c->cur;
     c->t++;
     c->halo_valid = false;
@@ -499,7 +504,63 @@ void after_sweep(iblb_ctx* c) {
     c->halo_valid = false;
 }
 
-// K = sweep_depth iterations in one launch (lone slab only; slabs of a group keep the 2-step halo)
+// K = sweep_depth iterations per cycle on a slab of an RCCL group (ncol >= 2K): the deep halo
+// (deep_slots(K) column-planes per side) exchanged and the boundary sweeps (output columns
+// [0, K) and [ncol-K, ncol), which then pack the deep halo of the new state) on the comm stream
+// beside the interior sweep [K, ncol-K), as sweep_step does for two iterations:
+//   comm:    exchange(t) -> wait int(t-K) -> boundary(t) -> pack halo(t+K) -> ev_bnd
+//   compute: (join_comm: boundary(t-K)) -> interior(t) -> ev_int
+template <typename T>
+int deep_slab_step(iblb_ctx* c) {
+    const int K = c->sweep_depth;
+    const int W = std::max(1, c->deep_w);
+    int rc = join_comm(c);
+    if (rc) return rc;
+    if (c->send_deep != K) {  // the send buffers hold another halo: pack the deep one now
+        HIP_TRY(c, launch_pack_deep_halo<T>(gptr<T>(c, c->cur), c->L, K, (T*)c->send_left, (T*)c->send_right,
+                                            c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+    }
+    const bool ov = c->overlap;
+    hipStream_t bs = ov ? c->comm_stream : c->stream;
+    if (!ov) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
+    if ((rc = exchange_rccl(c, bs, false, false, deep_slots(K)))) return rc;
+    if (ov) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
+    Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
+    b.vs = c->deep_vs;
+    b.variant = c->deep_variant;
+    if (b.map == 0) b.map = 2;
+    HIP_TRY(c, launch_sweepk<T>(b, K, true, bs));
+    HIP_TRY(c, launch_pack_deep_halo<T>(gptr<T>(c, 1 - c->cur), c->L, K, (T*)c->send_left, (T*)c->send_right, bs));
+    if (ov) HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
+    const int ni = c->ncol - 2 * K;  // interior [K, ncol-K): needs nothing from the halo
+    if (ni > 0) {
+        Sweep2Args<T> a = sweep_args<T>(c, K, c->deep_balance ? 0 : W, c->ncol - K, (ni + W - 1) / W, W);
+        a.vs = c->deep_vs;
+        a.variant = c->deep_variant;
+        if (a.map == 0) a.map = 2;
+        size_t ev = 0;
+        if ((rc = ev_begin(c, &ev, c->stream))) return rc;
+        HIP_TRY(c, launch_sweepk<T>(a, K, false, c->stream));
+        if ((rc = ev_end(c, ev, EV_SWEEPK, (long long)ni * c->ny, c->stream))) return rc;
+    }
+    if (ov) HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+    else {
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+    }
+    c->cur = 1 - c->cur;
+    c->t += K;
+    c->halo_valid = false;
+    c->send_sweep = false;
+    c->send_deep = K;
+    return IBLB_OK;
+}
+
+// K = sweep_depth iterations in one launch on a lone slab
 template <typename T>
 int sweepk_step(iblb_ctx* c) {
     const int W = std::max(1, c->deep_w);
@@ -511,7 +572,7 @@ int sweepk_step(iblb_ctx* c) {
     size_t ev = 0;
     int rc = ev_begin(c, &ev, c->stream);
     if (rc) return rc;
-    HIP_TRY(c, launch_sweepk<T>(a, c->sweep_depth, c->stream));
+    HIP_TRY(c, launch_sweepk<T>(a, c->sweep_depth, false, c->stream));
     if ((rc = ev_end(c, ev, EV_SWEEPK, (long long)c->ncol * c->ny, c->stream))) return rc;
     c->cur = 1 - c->cur;
     c->t += c->sweep_depth;
@@ -557,6 +618,7 @@ int sweep_step(iblb_ctx* c) {
         HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
         after_sweep(c);
         c->send_sweep = true;
+        c->send_deep = 0;
         return IBLB_OK;
     }
     if (!ov) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
@@ -576,6 +638,7 @@ int sweep_step(iblb_ctx* c) {
     }
     after_sweep(c);
     c->send_sweep = true;
+    c->send_deep = 0;
     return IBLB_OK;
 }
 
@@ -777,10 +840,14 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->sweep_variant = (int)env_long("IBLB_SWEEP_VARIANT", 1);
     c->sweep_map = (int)env_long("IBLB_SWEEP_MAP", 2);
     c->sweep_alt = (int)env_long("IBLB_SWEEP_ALT", 1);
-    c->sweep_depth = (int)env_long("IBLB_SWEEP_DEPTH", 2);
-    if (c->sweep_depth > 4) c->sweep_depth = 4;
-    c->deep_w = (int)env_long("IBLB_DEEP_W", 4);
-    c->deep_vs = (int)env_long("IBLB_DEEP_VS", c->prec == IBLB_PREC_F64 ? 2 : 4);
+    // deep sweeps (K = 3 .. 6 iterations per launch), measured on MI355X at 4096^2
+    // (profiles/r01d5_tune_deep_*.log): f64 K = 5, 2 cells per lane, ~96-column sweeps 0.142
+    // ms/iteration (118k MLUPS; K = 2: 0.227); f32 K = 5, one cell per lane, ~64 columns 0.095
+    // (177k; K = 2: 0.124).  Widths are balanced to whole rounds of resident waves.
+    c->sweep_depth = (int)env_long("IBLB_SWEEP_DEPTH", 5);
+    if (c->sweep_depth > 6) c->sweep_depth = 6;
+    c->deep_w = (int)env_long("IBLB_DEEP_W", c->prec == IBLB_PREC_F64 ? 96 : 64);
+    c->deep_vs = (int)env_long("IBLB_DEEP_VS", c->prec == IBLB_PREC_F64 ? 2 : 1);
     c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", 1);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     if (c->cfg.flux_column < 0) c->cfg.flux_column = c->nx - 5;
@@ -838,6 +905,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     // slots + guards
     {
         c->halo_slots = c->max_points > 0 ? IB_HALO_SLOTS : SWEEP_HALO_SLOTS;
+        if (c->sweep_depth >= 3) c->halo_slots = std::max(c->halo_slots, deep_slots(c->sweep_depth));
         const size_t slot = (size_t)(c->halo_slots * rows + 2 * GUARD) * c->esize;
         int rc = alloc_zero(c, (void**)&c->halo_alloc, 4 * slot);
         if (rc) return bail(rc);
@@ -1043,10 +1111,17 @@ int iblb_step(iblb_ctx* c, int nsteps) {
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
     for (int s = 0; s < nsteps;) {
-        if (c->sweep_depth >= 3 && nsteps - s >= c->sweep_depth && single_slab(c) && sweep_ready(c)) {
-            if ((rc = c->prec == IBLB_PREC_F64 ? sweepk_step<double>(c) : sweepk_step<float>(c))) return rc;
-            s += c->sweep_depth;
-            continue;
+        if (c->sweep_depth >= 3 && nsteps - s >= c->sweep_depth && sweep_ready(c)) {
+            if (single_slab(c)) {
+                if ((rc = c->prec == IBLB_PREC_F64 ? sweepk_step<double>(c) : sweepk_step<float>(c))) return rc;
+                s += c->sweep_depth;
+                continue;
+            }
+            if (rccl_multi(c) && c->ncol >= 2 * c->sweep_depth) {
+                if ((rc = c->prec == IBLB_PREC_F64 ? deep_slab_step<double>(c) : deep_slab_step<float>(c))) return rc;
+                s += c->sweep_depth;
+                continue;
+            }
         }
         if (nsteps - s >= 2 && sweep_ready(c)) {
             if ((rc = c->prec == IBLB_PREC_F64 ? sweep_step<double>(c) : sweep_step<float>(c))) return rc;

@@ -129,6 +129,24 @@ __host__ __device__ constexpr int send_slot_plane(bool to_right, int s) {
                           : (s < 18 ? s - 9 : (to_right ? left_plane(s - 18) : right_plane(s - 18))));
 }
 
+// ---- deep halo (K-iteration sweeps across slabs, K = 3 .. 6) --------------------------------
+// The IB halo generalised to depth K: d = 0 as ib_slot (streamed planes first, so slots 0-2 are
+// the one-step halo), d = 1 .. K-2 all nine planes, d = K-1 the streamed planes only.  For K = 3
+// it is exactly the IB halo.
+__host__ __device__ constexpr int deep_slots(int K) { return 9 * (K - 1) + 3; }
+__host__ __device__ constexpr int deep_slot(bool left, int d, int k, int K) {
+    if (d == 0) return ib_slot(left, 0, k);
+    if (d < K - 1) return 9 * d + k;
+    const bool streamed = left ? cx(k) == 1 : cx(k) == -1;
+    return (d == K - 1 && streamed) ? 9 * (K - 1) + halo_slot(k) : -1;
+}
+// the sender's view of slot s: column offset d from its edge and plane
+__host__ __device__ constexpr int deep_send_depth(int s, int K) { return s < 9 ? 0 : (s < 9 * (K - 1) ? s / 9 : K - 1); }
+__host__ __device__ constexpr int deep_send_plane(bool to_right, int s, int K) {
+    return s < 9 ? send_slot_plane(to_right, s)
+                 : (s < 9 * (K - 1) ? s % 9 : (to_right ? left_plane(s - 9 * (K - 1)) : right_plane(s - 9 * (K - 1))));
+}
+
 template <typename T>
 struct IbHalo {
     const T* left;   // received from the left neighbour, IB_HALO_SLOTS slots of `col` elements

@@ -85,10 +85,14 @@ struct Sweep2Args {
 // slab (periodic images) or interior columns of a group slab (no halo, no sends)
 template <typename T>
 hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s);
-// K = depth (3 or 4) iterations per launch on a lone slab (periodic columns): g^t -> g^{t+K};
-// map 1 or 2.
+// K = depth (3 .. 6) iterations per launch: g^t -> g^{t+K}; map 1 or 2.  slab = false: lone
+// slab (periodic columns) or interior columns of a group slab; slab = true: columns beyond the
+// edges from the deep halo (deep_slot) in recv_left / recv_right.  col_step 0: balanced widths.
 template <typename T>
-hipError_t launch_sweepk(Sweep2Args<T> a, int depth, hipStream_t s);
+hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool slab, hipStream_t s);
+// The deep halo of depth K of state g into both send buffers.
+template <typename T>
+hipError_t launch_pack_deep_halo(const T* g, Layout L, int depth, T* send_left, T* send_right, hipStream_t st);
 // The 2-step halo of state g into both send buffers (after a one-step launch or an IB exchange).
 template <typename T>
 hipError_t launch_pack_sweep_halo(const T* g, Layout L, T* send_left, T* send_right, hipStream_t st);

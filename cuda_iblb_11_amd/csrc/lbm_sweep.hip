@@ -389,7 +389,7 @@ hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
-// ---- K iterations per launch (lone slab, K = 3 or 4) ------------------------------------------
+// ---- K iterations per launch (lone slab, K = 3 .. 6) ------------------------------------------
 // sweepk_kernel: g^t -> g^{t+K}, the walk keeping K-1 register windows (g^{t+1} .. g^{t+K-1}).
 // Same wave geometry, order and walking directions as sweep2_kernel.  Valid rows shrink by one
 // per level at the wave's edges (the +-1-row pulls of the end lanes take garbage from level 2
@@ -415,24 +415,34 @@ __device__ __forceinline__ const T* col_periodic(const Sweep2Args<T>& a, int x, 
     return a.src + (long)xw * a.L.col + (long)k * a.L.plane;
 }
 
-template <typename T, int VS, int MODE>
+// plane k of column x for the deep walk: a lone slab wraps periodically; a slab of a group
+// (SLAB) reads columns beyond its edges from the deep halo (deep_slot, K columns per side)
+template <typename T, bool SLAB, int K>
+__device__ __forceinline__ const T* col_deep(const Sweep2Args<T>& a, int x, int k) {
+    if (!SLAB) return col_periodic<T>(a, x, k);
+    if (x < 0) return a.recv_left + (long)deep_slot(true, -1 - x, k, K) * a.L.rows;
+    if (x >= a.L.ncol) return a.recv_right + (long)deep_slot(false, x - a.L.ncol, k, K) * a.L.rows;
+    return a.src + (long)x * a.L.col + (long)k * a.L.plane;
+}
+
+template <typename T, int VS, int MODE, bool SLAB, int K>
 __device__ __forceinline__ void load_raw_periodic(const Sweep2Args<T>& a, int x, int row0, unsigned off, bool bot,
                                                   bool top, Raw<T, VS>& r) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
-        const T* p = col_periodic<T>(a, x - cx(k), k) + row0;
+        const T* p = col_deep<T, SLAB, K>(a, x - cx(k), k) + row0;
         ld_rows<T, VS, MODE>(p, off, r.v[k]);
         if (cy(k) == 1) r.e[k] = p[-1];
         if (cy(k) == -1) r.e[k] = p[64 * VS];
     }
     r.w[0] = r.w[1] = r.w[2] = r.w[3] = (T)0;
     if (bot) {
-        r.w[0] = col_periodic<T>(a, x, 7)[0];
-        r.w[1] = col_periodic<T>(a, x, 8)[0];
+        r.w[0] = col_deep<T, SLAB, K>(a, x, 7)[0];
+        r.w[1] = col_deep<T, SLAB, K>(a, x, 8)[0];
     }
     if (top) {
-        r.w[2] = col_periodic<T>(a, x, 5)[a.L.ny - 1];
-        r.w[3] = col_periodic<T>(a, x, 6)[a.L.ny - 1];
+        r.w[2] = col_deep<T, SLAB, K>(a, x, 5)[a.L.ny - 1];
+        r.w[3] = col_deep<T, SLAB, K>(a, x, 6)[a.L.ny - 1];
     }
 }
 
@@ -469,7 +479,7 @@ __device__ __forceinline__ void copy_col(T (&d)[9][VS], const T (&s)[9][VS]) {
         for (int e = 0; e < VS; ++e) d[k][e] = s[k][e];
 }
 
-template <typename T, int VS, int MODE, int K, bool REV>
+template <typename T, int VS, int MODE, int K, bool SLAB, bool REV>
 __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
                                               int lane, int r0, int et, bool owner, bool bot, bool top) {
     typedef typename Calc<T>::R R;
@@ -495,7 +505,7 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
         const int x = x0 + i * DX;
         const bool l1 = i < nl1;
         Raw<T, VS> cur;
-        if (l1) load_raw_periodic<T, VS, MODE>(a, x, row0, off, bot, top, cur);
+        if (l1) load_raw_periodic<T, VS, MODE, SLAB, K>(a, x, row0, off, bot, top, cur);
 
         // ---- levels 2 .. K of columns x - l*dx ----
         T N[9][VS];  // the column the previous level made in this iteration
@@ -567,7 +577,7 @@ template <int K, int VS>
 constexpr int ghost_lanes() { return (K - 1 + VS - 1) / VS; }
 
 // G ghost lanes at each wave edge (G * VS >= K - 1 rows)
-template <typename T, int VS, int MODE, int K>
+template <typename T, int VS, int MODE, int K, bool SLAB>
 __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     constexpr int G = ghost_lanes<K, VS>();
     constexpr int OWN = 64 - 2 * G;  // owned lanes per wave
@@ -594,8 +604,9 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     const bool bot = r0 == 0;
     const bool top = et >= 0 && et < VS;
     const double q = (a.alt && (sw & 1))
-                         ? sweepk_walk<T, VS, MODE, K, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
-                         : sweepk_walk<T, VS, MODE, K, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top);
+                         ? sweepk_walk<T, VS, MODE, K, SLAB, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
+                         : sweepk_walk<T, VS, MODE, K, SLAB, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot,
+                                                                     top);
     if (a.flux_col >= xa && a.flux_col < xb) {
         const double qs = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, qs);
@@ -603,28 +614,28 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
 }
 
 // Waves resident on the whole device for one instantiation (256-thread workgroups).
-template <typename T, int VS, int MODE, int K>
+template <typename T, int VS, int MODE, int K, bool SLAB>
 static long resident_waves() {
     static long cached = 0;
     if (cached) return cached;
     int dev = 0, ncu = 0, nb = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweepk_kernel<T, VS, MODE, K>, 256, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweepk_kernel<T, VS, MODE, K, SLAB>, 256, 0) != hipSuccess ||
         nb <= 0 || ncu <= 0)
         return 0;
     cached = (long)nb * 4 * ncu;
     return cached;
 }
 
-template <typename T, int VS, int MODE, int K>
+template <typename T, int VS, int MODE, int K, bool SLAB>
 static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s) {
     if (b.col_step <= 0) {
         // balanced sweeps: the wave count a whole number of device-wide rounds (the waves of one
         // launch all do the same work, so a partial last round idles the chip), sweeps close to
         // the requested W columns
         const long n = b.col_end - b.col_begin;
-        const long slots = resident_waves<T, VS, MODE, K>();
+        const long slots = resident_waves<T, VS, MODE, K, SLAB>();
         long ns = (n + b.W - 1) / b.W;
         if (slots > 0) {
             const long rounds = std::max(1L, (ns * b.nch + slots / 2) / slots);
@@ -633,43 +644,48 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s) {
         b.nsweep = (int)std::min(ns, n);
     }
     const unsigned blocks = (unsigned)(((long)b.nsweep * b.nch + 3) / 4);
-    sweepk_kernel<T, VS, MODE, K><<<blocks, 256, 0, s>>>(b);
+    sweepk_kernel<T, VS, MODE, K, SLAB><<<blocks, 256, 0, s>>>(b);
     return hipGetLastError();
 }
 
-template <typename T, int VS, int K>
+template <typename T, int VS, int K, bool SLAB>
 static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s) {
     constexpr int G = ghost_lanes<K, VS>();
     const int rows_per_wave = (64 - 2 * G) * VS;  // owned rows
     Sweep2Args<T> b = a;
     b.nch = (a.L.ny + rows_per_wave - 1) / rows_per_wave;
-    switch (a.variant) {
-        case 0: return launch_sweepk_mode<T, VS, 0, K>(b, s);
-        case 3: return launch_sweepk_mode<T, VS, 3, K>(b, s);
-        default: return launch_sweepk_mode<T, VS, 1, K>(b, s);
-    }
+    // variants: 1 = nontemporal stores (default), 0 = plain
+    if (a.variant == 0) return launch_sweepk_mode<T, VS, 0, K, SLAB>(b, s);
+    return launch_sweepk_mode<T, VS, 1, K, SLAB>(b, s);
 }
 
-template <typename T, int K>
+// cells per lane: 2 or 1 (4 in f32 measured slower: one wave per SIMD, profiles/r01d4_*)
+template <typename T, int K, bool SLAB>
 static hipError_t launch_sweepk_depth(const Sweep2Args<T>& a, hipStream_t s) {
-    constexpr int V = vec_of<T>();
-    if (a.vs == V) return launch_sweepk_vs<T, V, K>(a, s);
-    if (a.vs == V / 2) return launch_sweepk_vs<T, V / 2, K>(a, s);
-    if (V == 4 && a.vs == 1) return launch_sweepk_vs<T, 1, K>(a, s);
+    if (a.vs == 2) return launch_sweepk_vs<T, 2, K, SLAB>(a, s);
+    if (a.vs == 1) return launch_sweepk_vs<T, 1, K, SLAB>(a, s);
+    return hipErrorInvalidValue;
+}
+
+template <typename T, bool SLAB>
+static hipError_t launch_sweepk_slab(const Sweep2Args<T>& a, int depth, hipStream_t s) {
+    if (depth == 3) return launch_sweepk_depth<T, 3, SLAB>(a, s);
+    if (depth == 4) return launch_sweepk_depth<T, 4, SLAB>(a, s);
+    if (depth == 5) return launch_sweepk_depth<T, 5, SLAB>(a, s);
+    if (depth == 6) return launch_sweepk_depth<T, 6, SLAB>(a, s);
     return hipErrorInvalidValue;
 }
 
 template <typename T>
-hipError_t launch_sweepk(Sweep2Args<T> a, int depth, hipStream_t s) {
+hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool slab, hipStream_t s) {
     if (a.nsweep <= 0) return hipSuccess;
     // rows are read from row0 - 1 >= -(K-1) - VS - 1 to the last wave's row0 + 64*VS: inside the
     // 512-element guards of the buffers
     if (a.W <= 0 || a.L.ncol < 1 || a.vs <= 0 || a.map == 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 ||
         a.L.col % a.vs != 0)
         return hipErrorInvalidValue;
-    if (depth == 3) return launch_sweepk_depth<T, 3>(a, s);
-    if (depth == 4) return launch_sweepk_depth<T, 4>(a, s);
-    return hipErrorInvalidValue;
+    if (slab && (!a.recv_left || !a.recv_right)) return hipErrorInvalidValue;
+    return slab ? launch_sweepk_slab<T, true>(a, depth, s) : launch_sweepk_slab<T, false>(a, depth, s);
 }
 
 // 2-step halo of g into the send buffers (slot layout in iblb_kernels.h); one thread per
@@ -704,11 +720,39 @@ hipError_t launch_pack_sweep_halo(const T* g, Layout L, T* send_left, T* send_ri
     return hipGetLastError();
 }
 
+// deep halo of depth K of g into both send buffers (deep_slot layout); one thread per
+// (side, slot, row)
+template <typename T>
+__global__ void pack_deep_halo_kernel(const T* __restrict__ g, Layout L, int K, T* __restrict__ sl,
+                                      T* __restrict__ sr) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int ns = deep_slots(K);
+    const long per_side = (long)ns * L.ny;
+    if (idx >= 2 * per_side) return;
+    const bool to_left = idx < per_side;
+    const long i = to_left ? idx : idx - per_side;
+    const int s = (int)(i / L.ny), y = (int)(i - (long)s * L.ny);
+    const int d = deep_send_depth(s, K);
+    const int k = deep_send_plane(!to_left, s, K);
+    const int col = to_left ? d : L.ncol - 1 - d;
+    (to_left ? sl : sr)[(long)s * L.rows + y] = g[(long)col * L.col + (long)k * L.plane + y];
+}
+
+template <typename T>
+hipError_t launch_pack_deep_halo(const T* g, Layout L, int depth, T* send_left, T* send_right, hipStream_t st) {
+    if (depth < 3 || depth > 6 || L.ncol < depth) return hipErrorInvalidValue;
+    const long n = 2L * deep_slots(depth) * L.ny;
+    pack_deep_halo_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(g, L, depth, send_left, send_right);
+    return hipGetLastError();
+}
+
+template hipError_t launch_pack_deep_halo<double>(const double*, Layout, int, double*, double*, hipStream_t);
+template hipError_t launch_pack_deep_halo<float>(const float*, Layout, int, float*, float*, hipStream_t);
 template hipError_t launch_pack_sweep_halo<double>(const double*, Layout, double*, double*, hipStream_t);
 template hipError_t launch_pack_sweep_halo<float>(const float*, Layout, float*, float*, hipStream_t);
 template hipError_t launch_sweep2<double>(Sweep2Args<double>, bool, hipStream_t);
 template hipError_t launch_sweep2<float>(Sweep2Args<float>, bool, hipStream_t);
-template hipError_t launch_sweepk<double>(Sweep2Args<double>, int, hipStream_t);
-template hipError_t launch_sweepk<float>(Sweep2Args<float>, int, hipStream_t);
+template hipError_t launch_sweepk<double>(Sweep2Args<double>, int, bool, hipStream_t);
+template hipError_t launch_sweepk<float>(Sweep2Args<float>, int, bool, hipStream_t);
 
 }  // namespace iblb

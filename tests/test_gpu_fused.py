@@ -264,17 +264,19 @@ def test_errors_are_loud(gpu):
         slab.step(1)  # slab not linked to neighbours
 
 
-@pytest.mark.parametrize("n,with_ib,precision,overlap,bulk", [(2, False, "f64", 1, 0), (3, False, "f64", 1, 0),
-                                                              (3, False, "f64", 0, 0), (2, True, "f64", 1, 0),
-                                                              (4, True, "f64", 1, 0), (2, False, "f32", 1, 0),
-                                                              (2, False, "f64", 1, 1), (3, False, "f64", 1, 1),
-                                                              (3, False, "f64", 0, 1), (4, False, "f32", 1, 1)])
-def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap, bulk):
+@pytest.mark.parametrize("n,with_ib,precision,overlap,bulk,depth",
+                         [(2, False, "f64", 1, 0, 5), (3, False, "f64", 1, 0, 5), (3, False, "f64", 0, 0, 5),
+                          (2, True, "f64", 1, 0, 5), (4, True, "f64", 1, 0, 5), (2, False, "f32", 1, 0, 5),
+                          (2, False, "f64", 1, 1, 5), (3, False, "f64", 1, 1, 5), (3, False, "f64", 0, 1, 5),
+                          (4, False, "f32", 1, 1, 5), (2, False, "f64", 1, 1, 2), (3, False, "f32", 1, 1, 2),
+                          (3, False, "f64", 1, 1, 3), (4, False, "f64", 1, 1, 6)])
+def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap, bulk, depth):
     """The RCCL transport of iblb_ctx.hip (attach, halo send/recv pairing, node-value and
     flux all-reduces, collective readers) driven with N ranks as threads on the one GPU via
     the mock-RCCL test build (RCCL itself refuses two ranks on one device).  Without IB the
     decomposed run must be bit-identical to one slab; bulk: multi-step calls, i.e. the
-    two-iteration sweeps with the 2-step halo (boundary sweeps on the comm stream)."""
+    multi-iteration sweeps (depth 2: the 2-step halo; 3-6: the deep halo) with the boundary
+    sweeps on the comm stream."""
     import json
     import os
     import subprocess
@@ -282,7 +284,7 @@ def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap, bulk):
     here = os.path.dirname(os.path.abspath(__file__))
     cmd = [sys.executable, os.path.join(here, "mock_rccl", "run_group.py"), str(n), "48", "130", "25",
            "1" if with_ib else "0", precision, str(bulk)]
-    env = dict(os.environ, IBLB_OVERLAP=str(overlap))
+    env = dict(os.environ, IBLB_OVERLAP=str(overlap), IBLB_SWEEP_DEPTH=str(depth))
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert lines, p.stdout + p.stderr
@@ -434,14 +436,16 @@ def test_interleaved_layout_identical(gpu, monkeypatch, precision):
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("overlap", [1, 0])
-def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap):
+@pytest.mark.parametrize("depth", [2, 5])
+def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap, depth):
     """Bulk stepping of an RCCL group over real RCCL (self ring), readers interleaved: the
-    two-iteration sweeps with the 2-step halo (boundary sweeps on the comm stream beside the
-    interior sweep) and one-step launches for odd remainders; must equal the plain single slab
-    bit for bit."""
+    multi-iteration sweeps (depth 2: 2-step halo; depth 5: the deep halo, 39 column-planes per
+    side) with the boundary sweeps on the comm stream beside the interior sweep, shorter sweeps
+    and one-step launches for the remainders; must equal the plain single slab bit for bit."""
     from cuda_iblb_11_amd import workloads as W
     monkeypatch.setenv("IBLB_RCCL_SELF", "1")
     monkeypatch.setenv("IBLB_OVERLAP", str(overlap))
+    monkeypatch.setenv("IBLB_SWEEP_DEPTH", str(depth))
     nx, ny = 96, 200
     rho, u = W.perturbed_state(nx, ny, 8)
     ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 2e-7))
@@ -458,11 +462,15 @@ def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap):
         assert np.array_equal(r1, r2) and np.array_equal(u1, u2), n
     assert ring.steps == ref.steps == 107
     assert abs(ring.flux - ref.flux) <= 1e-13 * abs(ref.flux)  # per-chunk atomics: order varies
-    assert ring.timing()["sweep_launches"] >= 40  # the interior sweeps ran
+    tm = ring.timing()
+    if depth == 2:
+        assert tm["sweep_launches"] >= 40, tm  # the interior sweeps ran
+    else:
+        assert tm["sweepk_launches"] >= 15 and tm["sweepk_depth"] == depth, tm
     ring.close()
 
 
-@pytest.mark.parametrize("depth", [3, 4])
+@pytest.mark.parametrize("depth", [3, 4, 5, 6])
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
     """K = 3 or 4 iterations per launch (IBLB_SWEEP_DEPTH=K, lone slab: K-1 register windows,
@@ -472,7 +480,7 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
     ragged shapes including fewer columns than the K-column reach (periodic images wrap more
     than once).  1 + 10K + 2 steps = boot + 10 deep launches + one two-iteration launch."""
     from cuda_iblb_11_amd import workloads as W
-    vss = [2, 1] if precision == "f64" else [4, 2, 1]
+    vss = [2, 1]
     steps = 1 + 10 * depth + 2
     for nx, ny in [(37, 300), (2, 63), (5, 1100), (70, 125), (3, 130)]:
         rho, u = W.perturbed_state(nx, ny, 7)
@@ -485,7 +493,7 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
         monkeypatch.setenv("IBLB_SWEEP", "1")
         monkeypatch.setenv("IBLB_SWEEP_DEPTH", str(depth))
         for vs in vss:
-            for w, var, mp, alt, bal in [(4, 1, 2, 1, 0), (1, 0, 1, 0, 0), (3, 3, 2, 0, 1), (32, 1, 1, 1, 0),
+            for w, var, mp, alt, bal in [(4, 1, 2, 1, 0), (1, 0, 1, 0, 0), (3, 1, 2, 0, 1), (32, 1, 1, 1, 0),
                                          (7, 0, 2, 1, 1), (48, 1, 2, 1, 1)]:
                 monkeypatch.setenv("IBLB_DEEP_VS", str(vs))
                 monkeypatch.setenv("IBLB_DEEP_W", str(w))
@@ -517,6 +525,7 @@ def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch)
     62*VS), fewer columns than one sweep, one-row-above-a-chunk tops and several chunks; odd step
     counts end with a one-step launch.  Flux: same terms, other summation order."""
     from cuda_iblb_11_amd import workloads as W
+    monkeypatch.setenv("IBLB_SWEEP_DEPTH", "2")
     vss = [1, 2] if precision == "f64" else [2, 4]
     for nx, ny in [(37, 300), (5, 1100), (2, 63), (70, 125), (33, 249)]:
         rho, u = W.perturbed_state(nx, ny, 6)
@@ -547,7 +556,8 @@ def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch)
                     assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, mp, alt, float(np.max(np.abs(f - f_ref))))
                     assert abs(lat.flux - q_ref) <= 1e-12 * abs(q_ref), (lat.flux, q_ref)
                     lat.close()
-    for name in ("IBLB_SWEEP_VS", "IBLB_SWEEP_W", "IBLB_SWEEP_VARIANT", "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT"):
+    for name in ("IBLB_SWEEP_VS", "IBLB_SWEEP_W", "IBLB_SWEEP_VARIANT", "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT",
+                 "IBLB_SWEEP_DEPTH"):
         monkeypatch.delenv(name)
-    lat, sim = run_pair(gpu, oracle, 70, 125, 40, precision=precision)
+    lat, sim = run_pair(gpu, oracle, 70, 125, 40, precision=precision)  # default (deep) sweeps vs the oracle
     check_fields(lat, sim, TIGHT if precision == "f64" else TOL32)
