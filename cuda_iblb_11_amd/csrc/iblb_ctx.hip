@@ -64,7 +64,8 @@ struct iblb_ctx {
     bool sweep_on = true;
     int sweep_w = 4, sweep_vs = 2, sweep_variant = 1, sweep_map = 2, sweep_alt = 1;
     // K = 3 .. 6 iterations per launch on a lone slab (IBLB_SWEEP_DEPTH): columns per wave, cells per lane
-    int sweep_depth = 2, deep_w = 4, deep_vs = 2, deep_variant = 1, deep_balance = 1;
+    int sweep_depth = 2, deep_w = 4, deep_vs = 2, deep_variant = 1, deep_balance = 1, deep_bnd_vs = 2;
+    int reserved_cus = 0, ncu = 0;  // CUs kept free of the compute stream (RCCL groups), device CUs
     hipStream_t stream = nullptr;
     Coef coef{};
     // populations: two buffers in one allocation (deterministic relative placement of the
@@ -529,7 +530,7 @@ int deep_slab_step(iblb_ctx* c) {
     if ((rc = exchange_rccl(c, bs, false, false, deep_slots(K)))) return rc;
     if (ov) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
     Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
-    b.vs = c->deep_vs;
+    b.vs = c->deep_bnd_vs;
     b.variant = c->deep_variant;
     if (b.map == 0) b.map = 2;
     HIP_TRY(c, launch_sweepk<T>(b, K, true, bs));
@@ -539,6 +540,7 @@ int deep_slab_step(iblb_ctx* c) {
     if (ni > 0) {
         Sweep2Args<T> a = sweep_args<T>(c, K, c->deep_balance ? 0 : W, c->ncol - K, (ni + W - 1) / W, W);
         a.vs = c->deep_vs;
+        a.cus = c->ncu - c->reserved_cus;  // the compute stream's CU mask
         a.variant = c->deep_variant;
         if (a.map == 0) a.map = 2;
         size_t ev = 0;
@@ -850,6 +852,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->deep_vs = (int)env_long("IBLB_DEEP_VS", c->prec == IBLB_PREC_F64 ? 2 : 1);
     c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", 1);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
+    c->deep_bnd_vs = (int)env_long("IBLB_DEEP_BND_VS", c->deep_vs);
     if (c->cfg.flux_column < 0) c->cfg.flux_column = c->nx - 5;
 
     const double tau = cfg->tau, tau2 = cfg->tau2, cs = 0.57735;
@@ -1444,24 +1447,42 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         // optionally, keep IBLB_RESERVE_CUS compute units free of the collide for them.
         // 8 reserved CUs: 512 x 4096 f64 slab step 0.070 ms vs 0.165 ms without (self-ring
         // rehearsal, profiles/r01e_gap_probe.txt); 4 or 16 are within 1 %
-        const long reserve = env_long("IBLB_RESERVE_CUS", 8);
+        hipDeviceProp_t prop;
+        HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
+        c->ncu = prop.multiProcessorCount;
+        long reserve = env_long("IBLB_RESERVE_CUS", 8);
+        if (c->sweep_depth >= 3 && env_long("IBLB_RESERVE_CUS", -1) < 0) {
+            // deep slabs: enough CUs for every wave of the two boundary sweeps to be resident
+            // at once (they walk K-1 columns more than they write and sit on the critical path of
+            // the comm stream: exchange -> boundary -> pack)
+            int nch = 0;
+            const int wpc = c->prec == IBLB_PREC_F64
+                                ? sweepk_geometry<double>(c->sweep_depth, c->deep_bnd_vs, c->deep_variant, true, c->ny, &nch)
+                                : sweepk_geometry<float>(c->sweep_depth, c->deep_bnd_vs, c->deep_variant, true, c->ny, &nch);
+            if (wpc > 0) reserve = std::min(64L, std::max(8L, (long)((2 * nch + wpc - 1) / wpc)));
+        }
         if (reserve > 0) {
-            hipDeviceProp_t prop;
-            HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
-            const int ncu = prop.multiProcessorCount;
+            const int ncu = c->ncu;
             if (reserve >= ncu) return fail(c, IBLB_ERR_ARG, "IBLB_RESERVE_CUS exceeds the compute units");
-            // reserved: CUs ncu-1, ncu-1-stride, ... (stride 32 spreads them over the XCDs if the
-            // mask numbers CUs XCD by XCD)
-            const long stride = std::max(1L, env_long("IBLB_RESERVE_STRIDE", 1));
+            // Which CUs: the mask numbers CUs XCD by XCD (ncu/8 per XCD) and the dispatcher deals
+            // workgroups round-robin over the XCDs that have enabled CUs, so a partly reserved
+            // XCD becomes the straggler of every launch (512 x 4096 deep slab: interior sweep
+            // 218 us with the top 18 CUs reserved, one round ~110 us).  IBLB_RESERVE_SPREAD=1
+            // (default) reserves the same number on every XCD (the count rounded up to a
+            // multiple of 8); 0 reserves the top CUs (whole XCDs when a multiple of ncu/8).
+            const bool spread = env_long("IBLB_RESERVE_SPREAD", 1) != 0 && ncu % 8 == 0;
+            if (spread) reserve = (reserve + 7) / 8 * 8;
+            if (reserve >= ncu) return fail(c, IBLB_ERR_ARG, "IBLB_RESERVE_CUS exceeds the compute units");
             std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
             for (int i = 0; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+            const int per_xcd = ncu / 8;
             for (long k = 0; k < reserve; ++k) {
-                const long i = ncu - 1 - k * stride;
-                if (i < 0) return fail(c, IBLB_ERR_ARG, "IBLB_RESERVE_CUS x IBLB_RESERVE_STRIDE exceeds the CUs");
+                const long i = spread ? (k % 8) * per_xcd + (per_xcd - 1 - k / 8) : ncu - 1 - k;
                 mask[(size_t)i / 32] &= ~(1u << (i % 32));
             }
             hipStream_t masked = nullptr;
             HIP_TRY(c, hipExtStreamCreateWithCUMask(&masked, (uint32_t)mask.size(), mask.data()));
+            c->reserved_cus = (int)reserve;
             HIP_TRY(c, hipStreamSynchronize(c->stream));
             (void)hipStreamDestroy(c->stream);
             c->stream = masked;

@@ -75,6 +75,7 @@ struct Sweep2Args {
     int map;             // 1: linear, chunk fastest; 0: 4 sweeps per workgroup, XCD-contiguous;
                          // 2: linear order in XCD-contiguous ranges (default)
     int alt;             // odd sweeps walk right to left (neighbours read their shared edges together)
+    int cus;             // deep sweeps, balanced widths: CUs the launch's stream may use (0 = all)
     int flux_col;        // local column sampled for Q (both iterations), or -1
     double flux_norm;
     double* Q;
@@ -90,6 +91,9 @@ hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s);
 // edges from the deep halo (deep_slot) in recv_left / recv_right.  col_step 0: balanced widths.
 template <typename T>
 hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool slab, hipStream_t s);
+// Resident waves per CU of a deep-sweep configuration; *nch = its row chunks for ny rows.
+template <typename T>
+int sweepk_geometry(int depth, int vs, int variant, bool slab, int ny, int* nch);
 // The deep halo of depth K of state g into both send buffers.
 template <typename T>
 hipError_t launch_pack_deep_halo(const T* g, Layout L, int depth, T* send_left, T* send_right, hipStream_t st);

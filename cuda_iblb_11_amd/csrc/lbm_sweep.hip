@@ -613,19 +613,25 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     }
 }
 
-// Waves resident on the whole device for one instantiation (256-thread workgroups).
+// Waves of one instantiation resident per CU (256-thread workgroups), and on `cus` CUs (0: all).
 template <typename T, int VS, int MODE, int K, bool SLAB>
-static long resident_waves() {
+static long waves_per_cu() {
     static long cached = 0;
     if (cached) return cached;
-    int dev = 0, ncu = 0, nb = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweepk_kernel<T, VS, MODE, K, SLAB>, 256, 0) != hipSuccess ||
-        nb <= 0 || ncu <= 0)
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweepk_kernel<T, VS, MODE, K, SLAB>, 256, 0) != hipSuccess ||
+        nb <= 0)
         return 0;
-    cached = (long)nb * 4 * ncu;
+    cached = (long)nb * 4;
     return cached;
+}
+template <typename T, int VS, int MODE, int K, bool SLAB>
+static long resident_waves(int cus) {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        return 0;
+    return waves_per_cu<T, VS, MODE, K, SLAB>() * (cus > 0 ? std::min(cus, ncu) : ncu);
 }
 
 template <typename T, int VS, int MODE, int K, bool SLAB>
@@ -635,7 +641,7 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s) {
         // launch all do the same work, so a partial last round idles the chip), sweeps close to
         // the requested W columns
         const long n = b.col_end - b.col_begin;
-        const long slots = resident_waves<T, VS, MODE, K, SLAB>();
+        const long slots = resident_waves<T, VS, MODE, K, SLAB>(b.cus);
         long ns = (n + b.W - 1) / b.W;
         if (slots > 0) {
             const long rounds = std::max(1L, (ns * b.nch + slots / 2) / slots);
@@ -675,6 +681,33 @@ static hipError_t launch_sweepk_slab(const Sweep2Args<T>& a, int depth, hipStrea
     if (depth == 6) return launch_sweepk_depth<T, 6, SLAB>(a, s);
     return hipErrorInvalidValue;
 }
+
+// resident waves per CU and waves per launch column-chunk geometry of one configuration (the
+// context sizes the CUs it reserves for the boundary sweeps with it)
+template <typename T, int K, bool SLAB>
+static int deep_geometry(int vs, int variant, int ny, int* nch) {
+    if (vs == 2) {
+        *nch = (ny + (64 - 2 * ghost_lanes<K, 2>()) * 2 - 1) / ((64 - 2 * ghost_lanes<K, 2>()) * 2);
+        return (int)(variant == 0 ? waves_per_cu<T, 2, 0, K, SLAB>() : waves_per_cu<T, 2, 1, K, SLAB>());
+    }
+    *nch = (ny + (64 - 2 * ghost_lanes<K, 1>()) - 1) / (64 - 2 * ghost_lanes<K, 1>());
+    return (int)(variant == 0 ? waves_per_cu<T, 1, 0, K, SLAB>() : waves_per_cu<T, 1, 1, K, SLAB>());
+}
+
+template <typename T>
+int sweepk_geometry(int depth, int vs, int variant, bool slab, int ny, int* nch) {
+    *nch = 0;
+    if (vs != 1 && vs != 2) return 0;
+    switch (depth) {
+        case 3: return slab ? deep_geometry<T, 3, true>(vs, variant, ny, nch) : deep_geometry<T, 3, false>(vs, variant, ny, nch);
+        case 4: return slab ? deep_geometry<T, 4, true>(vs, variant, ny, nch) : deep_geometry<T, 4, false>(vs, variant, ny, nch);
+        case 5: return slab ? deep_geometry<T, 5, true>(vs, variant, ny, nch) : deep_geometry<T, 5, false>(vs, variant, ny, nch);
+        case 6: return slab ? deep_geometry<T, 6, true>(vs, variant, ny, nch) : deep_geometry<T, 6, false>(vs, variant, ny, nch);
+        default: return 0;
+    }
+}
+template int sweepk_geometry<double>(int, int, int, bool, int, int*);
+template int sweepk_geometry<float>(int, int, int, bool, int, int*);
 
 template <typename T>
 hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool slab, hipStream_t s) {
