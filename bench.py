@@ -308,6 +308,10 @@ def main():
                 "bytes_per_cell": bytes_per_cell,
                 "cells_per_launch": cells_per_launch,
                 "iterations_per_launch": iters_per_launch,
+                # temporal blocking: the one-step algorithm needs bytes_per_cell per lattice update;
+                # the rate it would have to sustain for this MLUPS, against the HBM peak
+                "one_step_equivalent_gbps": round(mlups * 1e6 * bytes_per_cell / 1e9, 1),
+                "one_step_equivalent_frac": round(mlups * 1e6 * bytes_per_cell / 1e9 / HBM_PEAK_GBPS, 4),
                 "launch_ms": round(launch_ms, 5),
                 "launch_timing": ("HIP events in the timed region" if events_in_timed else
                                   f"HIP events over {min(a.steps, 100)} further steps after the timed region"),

@@ -1459,25 +1459,31 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
             const int wpc = c->prec == IBLB_PREC_F64
                                 ? sweepk_geometry<double>(c->sweep_depth, c->deep_bnd_vs, c->deep_variant, true, c->ny, &nch)
                                 : sweepk_geometry<float>(c->sweep_depth, c->deep_bnd_vs, c->deep_variant, true, c->ny, &nch);
-            if (wpc > 0) reserve = std::min(64L, std::max(8L, (long)((2 * nch + wpc - 1) / wpc)));
+            // whole XCDs (ncu / 8 CUs each): a partly reserved XCD is the straggler of every
+            // interior launch (self ring, deep slab 512 / 1024 / 2048 x 4096: 0.0376 / 0.0564 /
+            // 0.0953 ms/iteration with 32 CUs, 0.046 / 0.080 / 0.148 with 16, 0.049 / 0.087 /
+            // 0.164 with 40; profiles/r01e5_gap_probe_reserve.txt)
+            if (wpc > 0) {
+                const long need = std::max(8L, (long)((2 * nch + wpc - 1) / wpc));
+                const long xcd = std::max(1, c->ncu / 8);
+                reserve = std::min((long)c->ncu / 2, (need + xcd - 1) / xcd * xcd);
+            }
         }
         if (reserve > 0) {
             const int ncu = c->ncu;
             if (reserve >= ncu) return fail(c, IBLB_ERR_ARG, "IBLB_RESERVE_CUS exceeds the compute units");
-            // Which CUs: the mask numbers CUs XCD by XCD (ncu/8 per XCD) and the dispatcher deals
-            // workgroups round-robin over the XCDs that have enabled CUs, so a partly reserved
-            // XCD becomes the straggler of every launch (512 x 4096 deep slab: interior sweep
-            // 218 us with the top 18 CUs reserved, one round ~110 us).  IBLB_RESERVE_SPREAD=1
-            // (default) reserves the same number on every XCD (the count rounded up to a
-            // multiple of 8); 0 reserves the top CUs (whole XCDs when a multiple of ncu/8).
-            const bool spread = env_long("IBLB_RESERVE_SPREAD", 1) != 0 && ncu % 8 == 0;
-            if (spread) reserve = (reserve + 7) / 8 * 8;
+            // Which CUs: the top ones (the last XCD first).  The dispatcher deals workgroups
+            // round-robin over the XCDs, so for long launches only whole XCDs should be reserved
+            // (above); IBLB_RESERVE_LAYOUT=1 takes the same number from every XCD instead
+            // (measured slower: 0.0486 vs 0.0376 ms/iteration with 32, profiles/r01e4_*).
+            const bool xcd_major = env_long("IBLB_RESERVE_LAYOUT", 0) == 1 && ncu % 8 == 0;
+            if (xcd_major) reserve = (reserve + 7) / 8 * 8;
             if (reserve >= ncu) return fail(c, IBLB_ERR_ARG, "IBLB_RESERVE_CUS exceeds the compute units");
             std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
             for (int i = 0; i < ncu; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
             const int per_xcd = ncu / 8;
             for (long k = 0; k < reserve; ++k) {
-                const long i = spread ? (k % 8) * per_xcd + (per_xcd - 1 - k / 8) : ncu - 1 - k;
+                const long i = xcd_major ? (k % 8) * per_xcd + (per_xcd - 1 - k / 8) : ncu - 1 - k;
                 mask[(size_t)i / 32] &= ~(1u << (i % 32));
             }
             hipStream_t masked = nullptr;
