@@ -64,7 +64,7 @@ struct iblb_ctx {
     bool sweep_on = true;
     int sweep_w = 4, sweep_vs = 2, sweep_variant = 1, sweep_map = 2, sweep_alt = 1;
     // K = 3 .. 6 iterations per launch on a lone slab (IBLB_SWEEP_DEPTH): columns per wave, cells per lane
-    int sweep_depth = 2, deep_w = 4, deep_vs = 2, deep_variant = 1, deep_balance = 1, deep_bnd_vs = 2;
+    int sweep_depth = 2, deep_w = 4, deep_vs = 2, deep_variant = 1, deep_balance = 1, deep_bnd_vs = 2, deep_slab_vs = 1;
     int reserved_cus = 0, ncu = 0;  // CUs kept free of the compute stream (RCCL groups), device CUs
     hipStream_t stream = nullptr;
     Coef coef{};
@@ -539,8 +539,12 @@ int deep_slab_step(iblb_ctx* c) {
     const int ni = c->ncol - 2 * K;  // interior [K, ncol-K): needs nothing from the halo
     if (ni > 0) {
         Sweep2Args<T> a = sweep_args<T>(c, K, c->deep_balance ? 0 : W, c->ncol - K, (ni + W - 1) / W, W);
-        a.vs = c->deep_vs;
+        a.vs = c->deep_slab_vs;
         a.cus = c->ncu - c->reserved_cus;  // the compute stream's CU mask
+        // whole XCDs reserved: the workgroups are dealt over the remaining ones
+        const int per_xcd = std::max(1, c->ncu / 8);
+        if (c->reserved_cus % per_xcd == 0 && env_long("IBLB_DEEP_XCD_DEAL", 1))
+            a.xcds = 8 - c->reserved_cus / per_xcd;
         a.variant = c->deep_variant;
         if (a.map == 0) a.map = 2;
         size_t ev = 0;
@@ -852,7 +856,10 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->deep_vs = (int)env_long("IBLB_DEEP_VS", c->prec == IBLB_PREC_F64 ? 2 : 1);
     c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", 1);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
-    c->deep_bnd_vs = (int)env_long("IBLB_DEEP_BND_VS", c->deep_vs);
+    // slabs of an RCCL group: one cell per lane (self ring 512 / 1024 / 2048 x 4096: 0.0347 /
+    // 0.0542 / 0.0935 ms/iteration vs 0.0380 / 0.0568 / 0.0942 with two, profiles/r01e7_*)
+    c->deep_slab_vs = (int)env_long("IBLB_DEEP_SLAB_VS", 1);
+    c->deep_bnd_vs = (int)env_long("IBLB_DEEP_BND_VS", c->deep_slab_vs);
     if (c->cfg.flux_column < 0) c->cfg.flux_column = c->nx - 5;
 
     const double tau = cfg->tau, tau2 = cfg->tau2, cs = 0.57735;

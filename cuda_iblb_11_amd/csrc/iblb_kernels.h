@@ -76,6 +76,7 @@ struct Sweep2Args {
                          // 2: linear order in XCD-contiguous ranges (default)
     int alt;             // odd sweeps walk right to left (neighbours read their shared edges together)
     int cus;             // deep sweeps, balanced widths: CUs the launch's stream may use (0 = all)
+    int xcds;            // deep sweeps, map 2: XCDs the workgroups are dealt over (0 = 8)
     int flux_col;        // local column sampled for Q (both iterations), or -1
     double flux_norm;
     double* Q;

@@ -562,11 +562,14 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
 }
 
 // wave -> (sweep, chunk) of the linear order, optionally dealt to the XCDs in contiguous ranges
-__device__ __forceinline__ void linear_item(int map, int nch, int wv, int& sw, int& ch) {
+// (xcds: the XCDs the launch's workgroups are dealt over; a stream whose CU mask leaves whole
+// XCDs out deals over the others)
+__device__ __forceinline__ void linear_item(int map, int nch, int xcds, int wv, int& sw, int& ch) {
     int b = (int)blockIdx.x;
     if (map == 2) {
-        const int q = (int)gridDim.x / 8;
-        if (b < 8 * q) b = (b % 8) * q + b / 8;
+        const int nx = xcds > 0 ? xcds : 8;
+        const int q = (int)gridDim.x / nx;
+        if (b < nx * q) b = (b % nx) * q + b / nx;
     }
     const int gw = b * 4 + wv;
     sw = gw / nch;
@@ -584,7 +587,7 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int sw, ch;
-    linear_item(a.map, a.nch, wv, sw, ch);
+    linear_item(a.map, a.nch, a.xcds, wv, sw, ch);
     if (sw >= a.nsweep || ch >= a.nch) return;
     int xa, xb;
     if (a.col_step > 0) {
