@@ -205,51 +205,82 @@ __device__ __forceinline__ void moments(const R f[9], R& rho, R& mx, R& my) {
 //   f1_i = f_i - w+ (f+ - feq+) + F+  -  w- (f- - feq-) + F-
 //   f1_ibar = f_ibar - w+ (f+ - feq+) + F+ + w- (f- - feq-) - F-
 //   f1_0 = f_0 - w+ (f_0 - feq_0)                         (no F_0, as in the reference)
-// Algebraically identical to the reference; rounding differs at the 1e-16 level.
+// Algebraically identical to the reference; rounding differs at the 1e-16 level.  The constant
+// products (w+ w, w- w / cs^2, k w, k w / cs^4, k w / cs^2, w+/2, w-/2) are folded per weight
+// class, so a pair costs ~19 fp64 operations instead of ~28 (the multi-iteration kernels are
+// bound by fp64 issue, profiles/r01d5_*):
+//   A = w+ feq+ + F+ - (w+/2)(f_i + f_ibar),   B = w- feq- + F- - (w-/2)(f_i - f_ibar)
+//   f1_i = f_i + (A + B),   f1_ibar = f_ibar + (A - B)
 // DEV: f holds deviations h = f - w and drho = rho - 1 (float storage).
+__device__ __forceinline__ double fmaR(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ float fmaR(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
 template <typename R, bool DEV>
 __device__ __forceinline__ void collide(R f[9], R rho, R drho, R ux, R uy, R Fx, R Fy, const Coef& c) {
 #pragma clang fp contract(on)  // fuse within a statement only: the same FMAs in every kernel
     const R op = (R)c.omega_p, om = (R)c.omega_m;
     const R a1 = (R)c.inv_2cs2, a2 = (R)c.inv_2cs4, ics2 = (R)c.inv_cs2, ics4 = (R)c.inv_cs4;
+    const R kk = (R)c.kguo;
     const R usq = ux * ux + uy * uy;
     const R uF = ux * Fx + uy * Fy;
-    const R base = -usq * a1;  // even equilibrium part common to all i
-    const R kk = (R)c.kguo;
-    // rest population
+    const R base = -usq * a1;              // even equilibrium part common to all i
+    const R ebase = DEV ? base : (R)1 + base;
+    const R guF = -uF * ics2;
+    // rest population: f0 - op (f0 - feq0) = (1 - op) f0 + op feq0
     {
         const R w0 = (R)(4. / 9);
-        const R feq0 = DEV ? w0 * (drho + rho * base) : rho * w0 * ((R)1 + base);
-        f[0] = f[0] - op * (f[0] - feq0);
+        const R feq0 = DEV ? w0 * (drho + rho * base) : rho * w0 * ebase;
+        f[0] = fmaR((R)1 - op, f[0], op * feq0);
     }
-    const R guF = -uF * ics2;
+    // per weight class (axis w = 1/9, diagonal w = 1/36)
+    R Rp[2], Rm[2], Dp[2], Gc[2];
+#pragma unroll
+    for (int cl = 0; cl < 2; ++cl) {
+        const R w = cl == 0 ? (R)(1. / 9) : (R)(1. / 36);
+        Rp[cl] = rho * (op * w);
+        Rm[cl] = rho * (om * w * ics2);
+        Dp[cl] = DEV ? drho * (op * w) : (R)0;
+        Gc[cl] = guF * (kk * w);
+    }
+    const R hop = (R)0.5 * op, hom = (R)0.5 * om;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         const int a = p == 0 ? 1 : (p == 1 ? 2 : (p == 2 ? 5 : 6));
         const int b = p == 0 ? 3 : (p == 1 ? 4 : (p == 2 ? 7 : 8));
-        const R w = (R)wgt(a);
+        const int cl = p < 2 ? 0 : 1;
+        const R w = cl == 0 ? (R)(1. / 9) : (R)(1. / 36);
         const R cu = (R)cx(a) * ux + (R)cy(a) * uy;
         const R cF = (R)cx(a) * Fx + (R)cy(a) * Fy;
-        const R rw = rho * w;
-        const R feqp = DEV ? w * drho + rw * (base + cu * cu * a2) : rw * ((R)1 + base + cu * cu * a2);
-        const R feqm = rw * cu * ics2;
-        const R fp = (R)0.5 * (f[a] + f[b]);
-        const R fm = (R)0.5 * (f[a] - f[b]);
-        const R kw = kk * w;
-        const R Gp = kw * (guF + cu * cF * ics4);
-        const R Gm = kw * cF * ics2;
-        const R A = -op * (fp - feqp) + Gp;
-        const R B = -om * (fm - feqm) + Gm;
-        f[a] = f[a] + A + B;
-        f[b] = f[b] + A - B;
+        const R P = fmaR(Rp[cl], fmaR(cu * cu, a2, ebase), Dp[cl]);  // w+ feq+
+        const R M = Rm[cl] * cu;                                                        // w- feq-
+        const R Gp = fmaR(cu * cF, kk * w * ics4, Gc[cl]);                     // F+
+        const R Gm = cF * (kk * w * ics2);                                              // F-
+        const R s = f[a] + f[b];
+        const R d = f[a] - f[b];
+        const R A = fmaR(-hop, s, P + Gp);
+        const R B = fmaR(-hom, d, M + Gm);
+        f[a] = f[a] + (A + B);
+        f[b] = f[b] + (A - B);
     }
+}
+
+// 1/x: v_rcp (about single precision) refined by two Newton steps (within an ulp of the
+// correctly rounded quotient; ~5 fp64 operations instead of the ~12 of an IEEE division)
+__device__ __forceinline__ double recip(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+    return __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ float recip(float x) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(r, __builtin_fmaf(-x, r, 1.f), r);
 }
 
 // One cell of a collide-stream step: f = the pulled populations f^t (deviations if DEV),
 // force = body force + IB force of this cell (double).  rho and u^t = (sum c f + force/2)/rho
 // (ImmersedBoundary.cu:249-255) from f, then collide in place; returns u_x (flux sample).
 // Contraction is per statement (fp contract(on)), not left to the backend, so the one-step and
-// the two-iteration kernels round every cell identically whatever code surrounds them.
+// the multi-iteration kernels round every cell identically whatever code surrounds them.
 template <typename R, bool DEV>
 __device__ __forceinline__ R relax_cell(R f[9], double fx, double fy, const Coef& c) {
 #pragma clang fp contract(on)
@@ -258,7 +289,7 @@ __device__ __forceinline__ R relax_cell(R f[9], double fx, double fy, const Coef
     const R rho = DEV ? (R)1 + s : s;
     const R Fx = (R)fx;
     const R Fy = (R)fy;
-    const R inv = (R)1 / rho;
+    const R inv = recip(rho);
     const R ux = (mx + (R)0.5 * Fx) * inv;
     const R uy = (my + (R)0.5 * Fy) * inv;
     collide<R, DEV>(f, rho, s, ux, uy, Fx, Fy, c);
