@@ -847,13 +847,14 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->sweep_map = (int)env_long("IBLB_SWEEP_MAP", 2);
     c->sweep_alt = (int)env_long("IBLB_SWEEP_ALT", 1);
     // deep sweeps (K = 3 .. 6 iterations per launch), measured on MI355X at 4096^2
-    // (profiles/r01d5_tune_deep_*.log): f64 K = 5, 2 cells per lane, ~96-column sweeps 0.142
-    // ms/iteration (118k MLUPS; K = 2: 0.227); f32 K = 5, one cell per lane, ~64 columns 0.095
-    // (177k; K = 2: 0.124).  Widths are balanced to whole rounds of resident waves.
+    // (profiles/r01d5_tune_deep_*.log, r01g_tune_*.log): f64 K = 5, 2 cells per lane, ~96-column
+    // sweeps 0.133 ms/iteration (126k MLUPS; K = 2: 0.236, one-step 0.399); f32 K = 5, 2 cells
+    // per lane, ~64 columns 0.087 (193k; K = 2: 0.121).  Widths are balanced to whole rounds of
+    // resident waves.
     c->sweep_depth = (int)env_long("IBLB_SWEEP_DEPTH", 5);
     if (c->sweep_depth > 6) c->sweep_depth = 6;
     c->deep_w = (int)env_long("IBLB_DEEP_W", c->prec == IBLB_PREC_F64 ? 96 : 64);
-    c->deep_vs = (int)env_long("IBLB_DEEP_VS", c->prec == IBLB_PREC_F64 ? 2 : 1);
+    c->deep_vs = (int)env_long("IBLB_DEEP_VS", 2);
     c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", 1);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     // slabs of an RCCL group: one cell per lane (self ring 512 / 1024 / 2048 x 4096: 0.0347 /
