@@ -353,7 +353,9 @@ def test_checkpoint_restart(gpu, tmp_path, precision, ib):
     assert b.steps == steps
     r2, v2 = b.macro()
     if ib == "none":
-        assert np.array_equal(r1, r2) and np.array_equal(v1, v2) and b.flux == q1
+        # fields bit-identical; Q sums per-wave partials with atomics (order varies)
+        assert np.array_equal(r1, r2) and np.array_equal(v1, v2)
+        assert abs(b.flux - q1) <= 1e-13 * abs(q1), (b.flux, q1)
     else:
         assert np.max(np.abs(r1 - r2)) <= 1e-13 and np.max(np.abs(v1 - v2)) <= 1e-13
         assert abs(b.flux - q1) <= 1e-12 * abs(q1)
