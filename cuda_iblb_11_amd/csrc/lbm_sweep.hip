@@ -56,18 +56,19 @@ __device__ __forceinline__ T wall_val(const Sweep2Args<T>& a, int x, int k, int 
 }
 
 // rows y0 .. y0+VS-1 of plane pointer p shifted by one row: DIR = +1 -> rows y-1, DIR = -1 ->
-// rows y+1, built from the aligned values v of this lane's rows; the end lane takes `edge`
+// rows y+1, built from the aligned values v of this lane's rows; the end lane takes *edge (no
+// edge: the end lane keeps whatever the shift left, it is a ghost row whose value is not used)
 template <typename T, int VS, int DIR>
-__device__ __forceinline__ void shift_rows(const T v[VS], T edge, int lane, T r[VS]) {
+__device__ __forceinline__ void shift_rows(const T v[VS], const T* edge, int lane, T r[VS]) {
     if (DIR > 0) {
         T prev = lane_shift<+1>(v[VS - 1]);
-        if (lane == 0) prev = edge;
+        if (edge && lane == 0) prev = *edge;
         r[0] = prev;
 #pragma unroll
         for (int e = 1; e < VS; ++e) r[e] = v[e - 1];
     } else {
         T next = lane_shift<-1>(v[0]);
-        if (lane == 63) next = edge;
+        if (edge && lane == 63) next = *edge;
 #pragma unroll
         for (int e = 0; e < VS - 1; ++e) r[e] = v[e + 1];
         r[VS - 1] = next;
@@ -156,9 +157,9 @@ __device__ __forceinline__ void pull_window(const T (*pk[9])[VS], const T* edge,
 #pragma unroll
             for (int e = 0; e < VS; ++e) s[k][e] = (*pk[k])[e];
         } else if (cy(k) == 1) {
-            shift_rows<T, VS, +1>(*pk[k], edge ? edge[k] : (T)0, lane, s[k]);
+            shift_rows<T, VS, +1>(*pk[k], edge ? edge + k : nullptr, lane, s[k]);
         } else {
-            shift_rows<T, VS, -1>(*pk[k], edge ? edge[k] : (T)0, lane, s[k]);
+            shift_rows<T, VS, -1>(*pk[k], edge ? edge + k : nullptr, lane, s[k]);
         }
     }
     if (r0 == 0) {  // bounce-back on y = 0 (LatticeBoltzmann.cu:328-340)
