@@ -123,6 +123,19 @@ def cpu_baseline(nx, ny, budget_s, points=None):
                       f"{dt:.1f} s"}
 
 
+def pmc_valu(workload_key):
+    """VALU figures of the dominant kernel per launch (profiles/pmc_valu.json, scripts/pmc_valu.py)."""
+    try:
+        return json.load(open(os.path.join(REPO, "profiles", "pmc_valu.json"))).get(workload_key)
+    except Exception:
+        return None
+
+
+# vector peaks: FP32 157.3 TFLOP/s (MI355X_MICROARCH.md); FP64 vector 78.6 TFLOP/s (AMD's MI355X
+# specification; half the FP32 vector rate)
+VALU_PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}
+
+
 def pmc_traffic(workload_key):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -261,6 +274,7 @@ def main():
     achieved = bytes_per_cell * cells_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else None
     key = f"{precision}_{nx}x{ny}_n{world}" + (f"_ib{ns}" if ns else "") + (f"_sweep{sweep}" if sweep not in (False, True) else ("_sweep" if sweep else ""))
     traffic, traffic_src = pmc_traffic(key)
+    valu = pmc_valu(key)
 
     if rank == 0:
         cpu = None
@@ -317,6 +331,13 @@ def main():
                                   f"HIP events over {min(a.steps, 100)} further steps after the timed region"),
                 "traffic_source": traffic_src,
             },
+            # the temporally blocked kernels are bound by vector issue, not HBM: their fp64 / fp32
+            # FLOP rate from the PMC FLOP count of a profiled pass over the measured launch time
+            "valu": (None if valu is None or launch_ms <= 0 else {
+                "achieved": round(valu["flops_per_launch"] / (launch_ms * 1e-3) / 1e12, 2),
+                "peak": VALU_PEAK_TFLOPS[precision], "unit": "TFLOP/s",
+                "frac": round(valu["flops_per_launch"] / (launch_ms * 1e-3) / 1e12 / VALU_PEAK_TFLOPS[precision], 4),
+                "valu_issue_share": valu.get("valu_issue_share"), "source": valu.get("source")}),
             "cpu_baseline": cpu,
             "state_finite": finite,
         }
