@@ -437,9 +437,9 @@ def test_interleaved_layout_identical(gpu, monkeypatch, precision):
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-@pytest.mark.parametrize("overlap", [1, 0])
+@pytest.mark.parametrize("overlap,order", [(1, 0), (0, 0), (1, 1)])
 @pytest.mark.parametrize("depth", [2, 5])
-def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap, depth):
+def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap, order, depth):
     """Bulk stepping of an RCCL group over real RCCL (self ring), readers interleaved: the
     multi-iteration sweeps (depth 2: 2-step halo; depth 5: the deep halo, 39 column-planes per
     side) with the boundary sweeps on the comm stream beside the interior sweep, shorter sweeps
@@ -448,6 +448,8 @@ def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap, depth):
     monkeypatch.setenv("IBLB_RCCL_SELF", "1")
     monkeypatch.setenv("IBLB_OVERLAP", str(overlap))
     monkeypatch.setenv("IBLB_SWEEP_DEPTH", str(depth))
+    monkeypatch.setenv("IBLB_SWEEP_ORDER", str(order))  # host submission order (interior first)
+    monkeypatch.setenv("IBLB_DEEP_ORDER", str(order))
     nx, ny = 96, 200
     rho, u = W.perturbed_state(nx, ny, 8)
     ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 2e-7))
