@@ -243,7 +243,9 @@ def main():
     # dominant kernel: the two-iteration sweep where it runs (no IB owed between iterations).
     # One sweep launch reads and writes the state once (the same 144 B/cell in f64) and
     # advances its cells by two iterations.
-    sweep = tm["sweep_launches"] > 0 and tm["sweep_launches"] >= tm["fused_launches"]
+    # (by summed launch time: with IB bands, five one-step launches over the band columns run
+    # beside one deep launch over the rest of the lattice per cycle)
+    sweep = tm["sweep_launches"] > 0 and tm["sweep_ms"] >= tm["fused_ms"]
     iters_per_launch = 1
     if sweep:
         launch_ms = tm["sweep_ms"] / tm["sweep_launches"]
@@ -254,7 +256,7 @@ def main():
         cells_per_launch = tm["sweep_cells"] // tm["sweep_launches"]
         iters_per_launch = 2
     # K >= 3 iterations per launch (lone slab, IBLB_SWEEP_DEPTH=K)
-    if tm["sweepk_launches"] > 0 and tm["sweepk_launches"] >= max(tm["sweep_launches"], tm["fused_launches"]):
+    if tm["sweepk_launches"] > 0 and tm["sweepk_ms"] >= max(tm["sweep_ms"], tm["fused_ms"]):
         sweep = int(tm["sweepk_depth"])
         launch_ms = tm["sweepk_ms"] / tm["sweepk_launches"]
         cells_per_launch = tm["sweepk_cells"] // tm["sweepk_launches"]
@@ -300,12 +302,21 @@ def main():
                             + (f"{iters_per_launch} iterations per launch (pull-stream+collide {iters_per_launch} times, "
                                "intermediate states in registers)" if sweep else
                                "one fused pull-stream+collide launch per step")
-                            + (f"; IB: {ns} static Lagrangian points, interpolate+spread every step" if ns else ""),
+                            + (f"; IB: {ns} static Lagrangian points, interpolate+spread every step" if ns else "")
+                            + ("; IB band cycle: columns within K-1 of a forced column one iteration per launch, "
+                               "the rest in the deep sweep" if ns and tm["sweepk_launches"] else ""),
                 "nx": nx, "ny": ny, "global_cells": cells, "ib_points": ns,
                 "parallelism": f"x-slab x{world}" + (" (RCCL halo)" if world > 1 else "")
                                + (" (RCCL self-ring rehearsal)" if a.rccl_self and world == 1 else ""),
             },
             "ib_ms_per_step": round(tm["ib_ms"] / a.steps, 5) if ns else None,
+            # IB band cycle (K iterations per cycle): lattice updates done by one-step launches over
+            # the band trapezoids (incl. their ghost columns) vs the deep sweep over the gaps
+            "ib_band": (None if not (ns and tm["sweepk_launches"]) else {
+                "one_step_lu": int(tm["fused_cells"]), "deep_lu": int(tm["sweepk_cells"] * tm["sweepk_depth"]),
+                "one_step_ms_per_cycle": round(tm["fused_ms"] / tm["sweepk_launches"], 5),
+                "deep_ms_per_cycle": round(tm["sweepk_ms"] / tm["sweepk_launches"], 5),
+                "ib_ms_per_cycle": round(tm["ib_ms"] / tm["sweepk_launches"], 5)}),
             # state bytes moved per second of the whole run (one read + one write per launch)
             "achieved_hbm_gbps": round(mlups * 1e6 * bytes_per_cell / iters_per_launch / 1e9, 1),
             "roofline": {

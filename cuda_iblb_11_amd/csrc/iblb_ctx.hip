@@ -98,6 +98,20 @@ struct iblb_ctx {
     float* d_Fs_sum = nullptr;  // F_s summed over an RCCL group (reader scratch)
     double* fdense = nullptr;
     uint8_t* flags = nullptr;
+    // IB bands of the K-iteration cycle (lone slab, points fixed between iblb_set_lagrangian
+    // calls): the columns an owed force can reach within K iterations advance one iteration per
+    // launch (trapezoid through sbuf), the force-free gaps between them in one deep sweep
+    int band_on = 1;                     // IBLB_IB_BAND
+    bool band_valid = false;
+    int* d_band = nullptr;               // level column tables, then the deep sweep table
+    size_t band_cap = 0;                 // ints allocated at d_band
+    std::vector<int> band_off, band_n;   // level j = 0 .. K-1: offset / columns in d_band
+    int band_sweep_off = 0, band_nsweep = 0;
+    long long band_deep_cols = 0, band_cols = 0;  // columns of the deep sweep / of all levels
+    int band_flux = -1;                  // flux column if a band outputs it, else -1
+    char* s_alloc = nullptr;             // two scratch population buffers of the trapezoid
+    void* sbuf[2] = {nullptr, nullptr};
+    long buf_elems = 0, buf_gap = 0;
     // flux: d_Q[0] cumulative, d_Q[1] scratch
     double* d_Q = nullptr;
     // state machine
@@ -170,6 +184,18 @@ bool single_slab(const iblb_ctx* c) {
 }
 bool rccl_multi(const iblb_ctx* c) { return c->transport == TR_RCCL && (c->nranks > 1 || c->self_ring); }
 bool ib_active(const iblb_ctx* c) { return c->max_points > 0 && c->ns > 0; }
+
+// periodic images of a lone slab: the edge columns of the buffer g itself
+template <typename T>
+Halo<T> halo_at(iblb_ctx* c, const T* g) {
+    Halo<T> H;
+    const Layout& L = c->L;
+    for (int p = 0; p < 3; ++p) {
+        H.left[p] = g + left_plane(p) * L.plane + (long)(L.ncol - 1) * L.col;
+        H.right[p] = g + right_plane(p) * L.plane;
+    }
+    return H;
+}
 
 template <typename T>
 Halo<T> halo_of(iblb_ctx* c, int which) {
@@ -390,6 +416,7 @@ int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, b
     a.col_begin = col_begin;
     a.col_step = col_step;
     a.ncols = ncols;
+    a.cols = nullptr;
     a.nch = c->nch;
     const bool ib = c->ib_state == IB_READY;
     a.flags = ib ? c->flags : nullptr;
@@ -605,6 +632,83 @@ int sweepk_step(iblb_ctx* c) {
     c->cur = 1 - c->cur;
     c->t += c->sweep_depth;
     c->halo_valid = false;
+    return IBLB_OK;
+}
+
+// ---- IB bands: K iterations per cycle with an owed force every iteration ---------------------
+// Lone slab, points fixed (iblb_set_lagrangian; not cilia).  The force of iteration t+j is
+// nonzero only in the forced columns F = [x0-1, x0+1] of the points, and the state of a column
+// x after K iterations depends on forces within K-1 columns of x.  So the output columns within
+// K-1 of F (the band) advance one iteration per launch over a shrinking trapezoid of columns
+// (level j = 0 .. K-1 covers the band +- (K-1-j) columns, from g^t through the scratch buffers,
+// the IB kernel evaluating force^{t+j} from level j-1 before it), and every other column in one
+// deep sweep g^t -> g^{t+K} (sweep table over the gaps).  Both read g^t and write disjoint
+// columns of g^{t+K}; each column is collided by the same kernels as one-step iterations, so the
+// result equals K one-step iterations (the deep sweep is bit-identical to them, the trapezoid
+// runs the one-step kernels themselves).
+bool band_ready(const iblb_ctx* c) {
+    return c->band_on && c->band_valid && single_slab(c) && c->phase == PH_RUN && !c->cilia_on && ib_active(c) &&
+           c->sweep_on && c->sweep_depth >= 3;
+}
+
+template <typename T>
+int band_step(iblb_ctx* c) {
+    const int K = c->sweep_depth;
+    int rc;
+    if (c->ib_state == IB_PENDING && (rc = ensure_force(c))) return rc;  // force^t from g^t
+    const T* A = gptr<T>(c, c->cur);
+    T* B = gptr<T>(c, 1 - c->cur);
+    T* S[2] = {(T*)c->sbuf[0], (T*)c->sbuf[1]};
+    // deep sweep over the force-free gaps first: the chip is full while it runs
+    if (c->band_nsweep > 0) {
+        Sweep2Args<T> d = sweep_args<T>(c, 0, 1, c->ncol, c->band_nsweep, std::max(1, c->deep_w));
+        d.sweep_tab = c->d_band + c->band_sweep_off;
+        d.vs = c->deep_vs;
+        d.variant = c->deep_variant;
+        if (d.map == 0) d.map = 2;
+        size_t ev = 0;
+        if ((rc = ev_begin(c, &ev, c->stream))) return rc;
+        HIP_TRY(c, launch_sweepk<T>(d, K, false, c->stream));
+        if ((rc = ev_end(c, ev, EV_SWEEPK, c->band_deep_cols * c->ny, c->stream))) return rc;
+    }
+    for (int j = 0; j < K; ++j) {
+        const T* src = j == 0 ? A : S[(j - 1) & 1];
+        T* dst = j == K - 1 ? B : S[j & 1];
+        if (j > 0) {  // force^{t+j} from the level below (valid on the band +- (K-j) columns)
+            size_t ev = 0;
+            if ((rc = ev_begin(c, &ev))) return rc;
+            HIP_TRY(c, launch_ib_point<T>(src, c->L, halo_at<T>(c, src), c->nx, c->ns, c->d_s, c->d_us, c->d_eps,
+                                          c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream));
+            if ((rc = ev_end(c, ev, EV_IB))) return rc;
+        }
+        FusedArgs<T> a;
+        a.src = src;
+        a.dst = dst;
+        a.L = c->L;
+        a.H = halo_at<T>(c, src);
+        for (int p = 0; p < 3; ++p) a.send_left[p] = a.send_right[p] = nullptr;
+        a.cols = c->d_band;
+        a.col_begin = c->band_off[j];
+        a.col_step = 1;
+        a.ncols = c->band_n[j];
+        a.nch = c->nch;
+        a.flags = c->flags;
+        a.fdense = c->fdense;
+        a.fplane = c->fplane;
+        a.flux_col = c->band_flux;  // ghost columns of the trapezoid never add flux
+        a.flux_norm = c->cfg.flux_norm;
+        a.Q = c->d_Q;
+        a.c = c->coef;
+        a.variant = c->variant;
+        size_t ev = 0;
+        if ((rc = ev_begin(c, &ev))) return rc;
+        HIP_TRY(c, launch_fused<T>(a, c->stream));
+        if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * c->ny))) return rc;
+    }
+    c->cur = 1 - c->cur;
+    c->t += K;
+    c->halo_valid = false;
+    c->ib_state = IB_PENDING;
     return IBLB_OK;
 }
 
@@ -933,7 +1037,10 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
         if (rc) return bail(rc);
         c->g[0] = c->g_alloc + GUARD * c->esize;
         c->g[1] = c->g_alloc + (GUARD + buf + gap) * c->esize;
+        c->buf_elems = buf;
+        c->buf_gap = gap;
     }
+    c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     // halo buffers: recv_left, recv_right, send_left, send_right; each 10 (2-step) or 21 (IB)
     // slots + guards
     {
@@ -975,7 +1082,7 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->ev_pre) (void)hipEventDestroy(c->ev_pre);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->g_alloc) (void)hipFree(c->g_alloc);
-    void* bufs[] = {c->cil_samples, c->cil_lasts, c->cil_bpoints,
+    void* bufs[] = {c->cil_samples, c->cil_lasts, c->cil_bpoints, c->s_alloc, c->d_band,
                     c->halo_alloc, c->rho0, c->u0, c->force0, c->d_s, c->d_us, c->d_Fs,
                     c->d_eps, c->d_Fs_sum, c->fdense, c->flags, c->d_Q};
     for (void* p : bufs)
@@ -1051,6 +1158,109 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
     return IBLB_OK;
 }
 
+}  // extern "C"
+
+// IB band plan of the points s (host copy) for band_step; band_valid stays false where the
+// cycle does not apply (see band_ready) or does not pay (bands over half the lattice, bands
+// within 2(K-1) columns of the lattice edge: the reference's flat-index wrap).
+template <typename T>
+static int plan_bands_t(iblb_ctx* c, int ns, const float* s) {
+    const int K = c->sweep_depth, nx = c->nx, R = 2 * (K - 1);
+    std::vector<std::pair<int, int>> f;
+    f.reserve((size_t)ns);
+    for (int k = 0; k < ns; ++k) {
+        const double x0 = std::nearbyint((double)s[2 * k]);
+        if (!(x0 - 1 - R >= 0. && x0 + 1 + R <= nx - 1.)) return IBLB_OK;
+        f.push_back({(int)x0 - 1, (int)x0 + 1});
+    }
+    std::sort(f.begin(), f.end());
+    std::vector<std::pair<int, int>> b;  // merged forced intervals: trapezoids apart, gaps >= R + 8
+    for (auto& iv : f) {
+        if (!b.empty() && iv.first - b.back().second - 1 < 2 * R + 8) b.back().second = std::max(b.back().second, iv.second);
+        else b.push_back(iv);
+    }
+    std::vector<int> tab;
+    std::vector<int> off((size_t)K), cnt((size_t)K);
+    long long cols = 0;
+    for (int j = 0; j < K; ++j) {
+        off[j] = (int)tab.size();
+        for (auto& iv : b)
+            for (int x = iv.first - R + j; x <= iv.second + R - j; ++x) tab.push_back(x);
+        cnt[j] = (int)tab.size() - off[j];
+        cols += cnt[j];
+    }
+    if (2 * cols > (long long)K * nx) return IBLB_OK;
+    // the gaps: columns farther than K-1 from every forced column
+    std::vector<std::pair<int, int>> gaps;
+    int prev = 0;
+    for (auto& iv : b) {
+        if (iv.first - (K - 1) > prev) gaps.push_back({prev, iv.first - (K - 1)});
+        prev = iv.second + K;
+    }
+    if (prev < nx) gaps.push_back({prev, nx});
+    long long ndeep = 0;
+    for (auto& g : gaps) ndeep += g.second - g.first;
+    // sweeps of ~deep_w columns, balanced to whole rounds of resident waves over the device
+    const int W = std::max(1, c->deep_w);
+    int nch = 0, ncu = 0;
+    const int wpc = sweepk_geometry<T>(K, c->deep_vs, c->deep_variant, false, c->ny, &nch);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+    long nsw = (long)((ndeep + W - 1) / W);
+    const long slots = (long)wpc * ncu;
+    if (c->deep_balance && slots > 0 && nch > 0 && ndeep > 0) {
+        const long rounds = std::max(1L, (nsw * nch + slots / 2) / slots);
+        nsw = std::max(1L, rounds * slots / nch);
+    }
+    const int sweep_off = (int)tab.size();
+    int nsweep = 0;
+    for (auto& g : gaps) {
+        const long w = g.second - g.first;
+        long n = std::max(1L, std::lround((double)nsw * (double)w / (double)ndeep));
+        n = std::min(n, w);
+        for (long k = 0; k < n; ++k) {
+            tab.push_back(g.first + (int)(k * w / n));
+            tab.push_back(g.first + (int)((k + 1) * w / n));
+            ++nsweep;
+        }
+    }
+    if (tab.size() > c->band_cap) {
+        if (c->d_band) (void)hipFree(c->d_band);
+        c->d_band = nullptr;
+        c->band_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_band, tab.size() * sizeof(int)));
+        c->band_cap = tab.size();
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpy(c->d_band, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (!c->s_alloc) {  // the trapezoid's scratch levels: two buffers laid out like g
+        const size_t bytes = (size_t)(2 * c->buf_elems + c->buf_gap + 2 * GUARD) * c->esize;
+        int rc = alloc_zero(c, (void**)&c->s_alloc, bytes);
+        if (rc) return rc;
+        c->sbuf[0] = c->s_alloc + GUARD * c->esize;
+        c->sbuf[1] = c->s_alloc + (GUARD + c->buf_elems + c->buf_gap) * c->esize;
+    }
+    c->band_off = off;
+    c->band_n = cnt;
+    c->band_sweep_off = sweep_off;
+    c->band_nsweep = nsweep;
+    c->band_deep_cols = ndeep;
+    c->band_cols = cols;
+    c->band_flux = -1;
+    const int fc = c->cfg.flux_column;
+    for (auto& iv : b)
+        if (fc >= iv.first - (K - 1) && fc <= iv.second + (K - 1)) c->band_flux = fc;
+    c->band_valid = true;
+    return IBLB_OK;
+}
+
+static int plan_bands(iblb_ctx* c, int ns, const float* s) {
+    c->band_valid = false;
+    if (!c->band_on || ns <= 0 || c->sweep_depth < 3 || !c->sweep_on || c->ncol != c->nx || c->cilia_on) return IBLB_OK;
+    return c->prec == IBLB_PREC_F64 ? plan_bands_t<double>(c, ns, s) : plan_bands_t<float>(c, ns, s);
+}
+
+extern "C" {
+
 int iblb_set_lagrangian(iblb_ctx* c, int ns, const float* s, const float* u_s, const int* epsilon) {
     if (!c || ns < 0) return IBLB_ERR_ARG;
     if (ns > c->max_points) return fail(c, IBLB_ERR_ARG, "ns exceeds max_points of the context");
@@ -1084,7 +1294,7 @@ int iblb_set_lagrangian(iblb_ctx* c, int ns, const float* s, const float* u_s, c
         HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
     c->ns = ns;
-    return IBLB_OK;
+    return plan_bands(c, ns, s);
 }
 
 static int reset_cilia_state(iblb_ctx* c) {
@@ -1098,6 +1308,7 @@ static int reset_cilia_state(iblb_ctx* c) {
 
 int iblb_set_cilia(iblb_ctx* c, const iblb_cilia* k) {
     if (!c) return IBLB_ERR_ARG;
+    c->band_valid = false;  // the points now come from the kinematics
     HIP_TRY(c, hipSetDevice(c->device));
     if (c->ib_state == IB_PENDING) {  // force still owed to the current points
         if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: set cilia between group steps");
@@ -1144,6 +1355,11 @@ int iblb_step(iblb_ctx* c, int nsteps) {
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
     for (int s = 0; s < nsteps;) {
+        if (nsteps - s >= c->sweep_depth && band_ready(c)) {
+            if ((rc = c->prec == IBLB_PREC_F64 ? band_step<double>(c) : band_step<float>(c))) return rc;
+            s += c->sweep_depth;
+            continue;
+        }
         if (c->sweep_depth >= 3 && nsteps - s >= c->sweep_depth && sweep_ready(c)) {
             if (single_slab(c)) {
                 if ((rc = c->prec == IBLB_PREC_F64 ? sweepk_step<double>(c) : sweepk_step<float>(c))) return rc;
@@ -1737,6 +1953,12 @@ int iblb_load_checkpoint(iblb_ctx* c, const char* path) {
         HIP_TRY(c, hipMemsetAsync(c->flags, 0, (size_t)c->ncol * c->nch, c->stream));
     }
     c->ns = (int)ns;
+    c->band_valid = false;
+    if (ns > 0 && !c->cilia_on) {  // the band plan of the restored points
+        std::vector<float> hs(2 * ns);
+        HIP_TRY(c, hipMemcpy(hs.data(), c->d_s, hs.size() * sizeof(float), hipMemcpyDeviceToHost));
+        if ((rc = plan_bands(c, (int)ns, hs.data()))) return rc;
+    }
     c->t = iv[CK_T];
     c->phase = PH_RUN;
     c->halo_valid = false;

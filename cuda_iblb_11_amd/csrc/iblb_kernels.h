@@ -23,6 +23,8 @@ struct FusedArgs {
     int col_begin;      // first local column handled by this launch
     int col_step;       // distance between the columns of this launch (1 = contiguous range)
     int ncols;          // columns handled by this launch
+    const int* cols;    // column table (device): column k of the launch is cols[col_begin + k]
+                        // (nullptr: col_begin + k * col_step); IB bands of the K-iteration cycle
     int nch;            // 64*V-row chunks per column
     uint8_t* flags;     // per (column, chunk): dense IB force present (nullptr: no IB); the
                         // wave that consumes a chunk's force clears its values and its flag
@@ -77,6 +79,8 @@ struct Sweep2Args {
     int alt;             // odd sweeps walk right to left (neighbours read their shared edges together)
     int cus;             // deep sweeps, balanced widths: CUs the launch's stream may use (0 = all)
     int xcds;            // deep sweeps, map 2: XCDs the workgroups are dealt over (0 = 8)
+    const int* sweep_tab;  // deep sweeps: sweep s covers [sweep_tab[2s], sweep_tab[2s+1]) (device;
+                           // nullptr: col_begin / col_step / W); the force-free gaps between IB bands
     int flux_col;        // local column sampled for Q (both iterations), or -1
     double flux_norm;
     double* Q;

@@ -21,7 +21,8 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (gw >= a.ncols * a.nch) return;
-    const int xc = a.col_begin + (gw / a.nch) * a.col_step;
+    const int xc = a.cols ? __builtin_amdgcn_readfirstlane(a.cols[a.col_begin + gw / a.nch])
+                          : a.col_begin + (gw / a.nch) * a.col_step;
     const int ch = gw - (gw / a.nch) * a.nch;
     const Layout L = a.L;
     const int cs = ch * (64 * V);

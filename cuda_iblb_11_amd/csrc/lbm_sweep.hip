@@ -591,7 +591,10 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     linear_item(a.map, a.nch, a.xcds, wv, sw, ch);
     if (sw >= a.nsweep || ch >= a.nch) return;
     int xa, xb;
-    if (a.col_step > 0) {
+    if (a.sweep_tab) {
+        xa = __builtin_amdgcn_readfirstlane(a.sweep_tab[2 * sw]);
+        xb = __builtin_amdgcn_readfirstlane(a.sweep_tab[2 * sw + 1]);
+    } else if (a.col_step > 0) {
         xa = a.col_begin + sw * a.col_step;
         xb = min(xa + a.W, a.col_end);
     } else {  // balanced: nsweep sweeps of floor/ceil((col_end - col_begin) / nsweep) columns
@@ -640,7 +643,7 @@ static long resident_waves(int cus) {
 
 template <typename T, int VS, int MODE, int K, bool SLAB>
 static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s) {
-    if (b.col_step <= 0) {
+    if (b.col_step <= 0 && !b.sweep_tab) {
         // balanced sweeps: the wave count a whole number of device-wide rounds (the waves of one
         // launch all do the same work, so a partial last round idles the chip), sweeps close to
         // the requested W columns

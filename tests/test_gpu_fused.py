@@ -565,3 +565,94 @@ def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch)
         monkeypatch.delenv(name)
     lat, sim = run_pair(gpu, oracle, 70, 125, 40, precision=precision)  # default (deep) sweeps vs the oracle
     check_fields(lat, sim, TIGHT if precision == "f64" else TOL32)
+
+
+# ---- IB bands: K iterations per cycle with a force owed every iteration (band_step) ----------
+def _static_run(P, O, nx, ny, steps, pts, *, precision="f64", body_force=(1e-6, 0.0), chunks=(None,), band=1,
+                monkeypatch=None, flux_column=None):
+    """Points fixed for the whole run (set once), lat.step(n) in the given chunk sizes: the band
+    cycle runs where n >= K; the oracle steps one reference iteration at a time."""
+    from cuda_iblb_11_amd import workloads as W
+    monkeypatch.setenv("IBLB_IB_BAND", str(band))
+    rho, u = W.perturbed_state(nx, ny, 11)
+    kw = {} if flux_column is None else {"flux_column": flux_column}
+    sim = O.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=body_force, **kw)
+    lat = P.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=body_force, max_points=4096, **kw)
+    lat.set_state(rho, u)
+    s, us, eps = pts
+    sim.set_lagrangian(s, us, eps)
+    lat.set_lagrangian(s, us, eps)
+    lat.set_profiling(True)
+    done = 0
+    for n in chunks:
+        n = steps - done if n is None else n
+        lat.step(n)
+        done += n
+    sim.step(steps)
+    return lat, sim
+
+
+def _line(xs, n, y0=3.0, dy=1.0, amp=1.5e-3):
+    k = np.arange(n)
+    s = np.empty(2 * n, dtype=np.float32)
+    s[0::2] = xs + 0.25 * np.sin(0.3 * k)
+    s[1::2] = y0 + dy * k
+    us = np.zeros(2 * n, dtype=np.float32)
+    us[0::2] = amp * (k / n)
+    us[1::2] = -0.3 * amp * np.cos(0.2 * k)
+    return s, us, (k % 7 != 3).astype(np.int32)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_ib_band_cycle_matches_oracle(gpu, oracle, precision, monkeypatch):
+    """Two filaments (two bands, one deep gap each side), 1 + 5*6 + 2 steps in one call: boot,
+    six band cycles, a one-step remainder; fields, force, F_s and the flux against the oracle."""
+    nx, ny = 256, 160
+    a, b = _line(64.37, 60), _line(171.6, 48, y0=20.0)
+    pts = tuple(np.concatenate([p, q]) for p, q in zip(a, b))
+    lat, sim = _static_run(gpu, oracle, nx, ny, 33, pts, precision=precision, monkeypatch=monkeypatch)
+    tm = lat.timing()
+    assert tm["sweepk_launches"] >= 6, tm  # the band cycle ran (one deep sweep per cycle)
+    tol = 1e-10 if precision == "f64" else TOL32
+    check_fields(lat, sim, tol)
+    assert rel(lat.force(), sim.force) <= (1e-9 if precision == "f64" else 1e-3)
+    assert rel(lat.lagrangian_force(), sim.F_s) <= (1e-5 if precision == "f64" else 1e-2)
+    assert abs(lat.flux - sim.flux) <= (1e-9 if precision == "f64" else 1e-4) * max(abs(sim.flux), 1e-30)
+
+
+@pytest.mark.parametrize("x0", [246.2, 243.8, 200.0])
+def test_ib_band_flux_column(gpu, oracle, x0, monkeypatch):
+    """Flux column XDIM-5 = 251 inside a band's output (x0 = 246), inside its trapezoid ghost
+    columns only (x0 = 244: the deep sweep adds it, the ghosts must not), and in a gap."""
+    nx, ny = 256, 128
+    lat, sim = _static_run(gpu, oracle, nx, ny, 20, _line(x0, 40), monkeypatch=monkeypatch)
+    assert lat.timing()["sweepk_launches"] >= 3
+    check_fields(lat, sim, 1e-10)
+    assert abs(lat.flux - sim.flux) <= 1e-9 * max(abs(sim.flux), 1e-30)
+
+
+def test_ib_band_equals_one_step_path(gpu, oracle, monkeypatch):
+    """The band cycle against the same run with IBLB_IB_BAND=0 (one-step launches only): equal up
+    to the arrival order of the spread atomics; the chunked calls (3, 5, 7, 5, 10) interleave band
+    cycles, one-step remainders and readers (macro, force) between them."""
+    nx, ny = 320, 96
+    pts = tuple(np.concatenate([p, q, r]) for p, q, r in zip(_line(40.0, 30), _line(60.0, 30), _line(200.4, 50)))
+    runs = {}
+    for band in (1, 0):
+        lat, sim = _static_run(gpu, oracle, nx, ny, 30, pts, chunks=(3, 5, 7, 5, 10), band=band,
+                               monkeypatch=monkeypatch)
+        runs[band] = (lat.macro(), lat.force(), lat.flux, lat.timing()["sweepk_launches"])
+    assert runs[1][3] >= 4 and runs[0][3] == 0
+    (r1, u1), (r0, u0) = runs[1][0], runs[0][0]
+    assert rel(r1, r0) <= 1e-13 and rel(u1, u0) <= 1e-12
+    assert rel(runs[1][1], runs[0][1]) <= 1e-12
+    check_fields(lat, sim, 1e-10)
+
+
+def test_ib_band_declined_near_edges(gpu, oracle, monkeypatch):
+    """Points within 2(K-1)+1 columns of x = 0 (the reference's flat-index wrap): no band plan,
+    the one-step path runs (no deep launch) and still matches the oracle."""
+    nx, ny = 128, 96
+    lat, sim = _static_run(gpu, oracle, nx, ny, 12, _line(3.4, 30), monkeypatch=monkeypatch)
+    assert lat.timing()["sweepk_launches"] == 0
+    check_fields(lat, sim, 1e-10)
