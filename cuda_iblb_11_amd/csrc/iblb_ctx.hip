@@ -112,6 +112,11 @@ struct iblb_ctx {
     char* s_alloc = nullptr;             // two scratch population buffers of the trapezoid
     void* sbuf[2] = {nullptr, nullptr};
     long buf_elems = 0, buf_gap = 0;
+    // the band chain beside the deep sweep: CUs reserved for it (whole XCDs, IBLB_BAND_RESERVE_CUS;
+    // 0 = both on the compute stream, in sequence)
+    int band_reserve = 0;
+    hipStream_t band_st = nullptr;
+    hipEvent_t ev_b0 = nullptr, ev_b2 = nullptr;
     // flux: d_Q[0] cumulative, d_Q[1] scratch
     double* d_Q = nullptr;
     // state machine
@@ -260,6 +265,7 @@ int ev_end(iblb_ctx* c, size_t idx, int kind, long long cells = 0, hipStream_t s
     if (c->ev_used >= 8192) {  // bound the pool: drain what is recorded
         HIP_TRY(c, hipEventSynchronize(c->ev_pool[idx + 1]));
         if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));
+        if (c->band_st) HIP_TRY(c, hipStreamSynchronize(c->band_st));
         for (auto& r : c->ev_kind) {
             float ms = 0.f;
             HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_pool[r.idx], c->ev_pool[r.idx + 1]));
@@ -655,10 +661,27 @@ template <typename T>
 int band_step(iblb_ctx* c) {
     const int K = c->sweep_depth;
     int rc;
-    if (c->ib_state == IB_PENDING && (rc = ensure_force(c))) return rc;  // force^t from g^t
     const T* A = gptr<T>(c, c->cur);
     T* B = gptr<T>(c, 1 - c->cur);
     T* S[2] = {(T*)c->sbuf[0], (T*)c->sbuf[1]};
+    // overlapped: the deep sweep on the compute stream (masked to the CUs outside the reserved
+    // XCDs), the band chain on band_st (the reserved XCDs).  The chain starts with the compute
+    // stream's work so far (deep sweep of the previous cycle included); the compute stream waits
+    // for the chain at the end of the cycle, after the deep sweep is queued.
+    const bool ov = c->band_st != nullptr;
+    hipStream_t bs = ov ? c->band_st : c->stream, ds = c->stream;
+    if (ov) {
+        HIP_TRY(c, hipEventRecord(c->ev_b0, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_b0, 0));
+    }
+    if (c->ib_state == IB_PENDING) {  // force^t from g^t
+        size_t ev = 0;
+        if ((rc = ev_begin(c, &ev, bs))) return rc;
+        HIP_TRY(c, launch_ib_point<T>(A, c->L, halo_at<T>(c, A), c->nx, c->ns, c->d_s, c->d_us, c->d_eps, c->d_Fs,
+                                      c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, bs));
+        if ((rc = ev_end(c, ev, EV_IB, 0, bs))) return rc;
+        c->ib_state = IB_READY;
+    }
     // deep sweep over the force-free gaps first: the chip is full while it runs
     if (c->band_nsweep > 0) {
         Sweep2Args<T> d = sweep_args<T>(c, 0, 1, c->ncol, c->band_nsweep, std::max(1, c->deep_w));
@@ -666,20 +689,22 @@ int band_step(iblb_ctx* c) {
         d.vs = c->deep_vs;
         d.variant = c->deep_variant;
         if (d.map == 0) d.map = 2;
+        const int per_xcd = std::max(1, c->ncu / 8);
+        if (ov && c->band_reserve % per_xcd == 0) d.xcds = 8 - c->band_reserve / per_xcd;
         size_t ev = 0;
-        if ((rc = ev_begin(c, &ev, c->stream))) return rc;
-        HIP_TRY(c, launch_sweepk<T>(d, K, false, c->stream));
-        if ((rc = ev_end(c, ev, EV_SWEEPK, c->band_deep_cols * c->ny, c->stream))) return rc;
+        if ((rc = ev_begin(c, &ev, ds))) return rc;
+        HIP_TRY(c, launch_sweepk<T>(d, K, false, ds));
+        if ((rc = ev_end(c, ev, EV_SWEEPK, c->band_deep_cols * c->ny, ds))) return rc;
     }
     for (int j = 0; j < K; ++j) {
         const T* src = j == 0 ? A : S[(j - 1) & 1];
         T* dst = j == K - 1 ? B : S[j & 1];
         if (j > 0) {  // force^{t+j} from the level below (valid on the band +- (K-j) columns)
             size_t ev = 0;
-            if ((rc = ev_begin(c, &ev))) return rc;
+            if ((rc = ev_begin(c, &ev, bs))) return rc;
             HIP_TRY(c, launch_ib_point<T>(src, c->L, halo_at<T>(c, src), c->nx, c->ns, c->d_s, c->d_us, c->d_eps,
-                                          c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream));
-            if ((rc = ev_end(c, ev, EV_IB))) return rc;
+                                          c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, bs));
+            if ((rc = ev_end(c, ev, EV_IB, 0, bs))) return rc;
         }
         FusedArgs<T> a;
         a.src = src;
@@ -701,9 +726,13 @@ int band_step(iblb_ctx* c) {
         a.c = c->coef;
         a.variant = c->variant;
         size_t ev = 0;
-        if ((rc = ev_begin(c, &ev))) return rc;
-        HIP_TRY(c, launch_fused<T>(a, c->stream));
-        if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * c->ny))) return rc;
+        if ((rc = ev_begin(c, &ev, bs))) return rc;
+        HIP_TRY(c, launch_fused<T>(a, bs));
+        if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * c->ny, bs))) return rc;
+    }
+    if (ov) {
+        HIP_TRY(c, hipEventRecord(c->ev_b2, bs));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b2, 0));
     }
     c->cur = 1 - c->cur;
     c->t += K;
@@ -1077,6 +1106,12 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    if (c->band_st) {
+        (void)hipStreamSynchronize(c->band_st);
+        (void)hipStreamDestroy(c->band_st);
+    }
+    for (hipEvent_t e : {c->ev_b0, c->ev_b2})
+        if (e) (void)hipEventDestroy(e);
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
     if (c->ev_int) (void)hipEventDestroy(c->ev_int);
     if (c->ev_pre) (void)hipEventDestroy(c->ev_pre);
@@ -1160,6 +1195,49 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
 
 }  // extern "C"
 
+// Streams of the overlapped band cycle (lone slab): the band chain on its own stream restricted
+// to `band_reserve` CUs (whole XCDs at the top, like the RCCL comm stream's), the compute stream
+// (deep sweeps, everything else) masked to the other CUs.  Default: one XCD, two where the band
+// trapezoids hold more than 5 % of the cycle's lattice updates (one-step launches, HBM-bound; the
+// deep sweep is issue-bound).  IBLB_BAND_RESERVE_CUS=0: both on the compute stream, in sequence.
+static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
+    if (c->transport != TR_NONE || c->comm_stream) return IBLB_OK;  // RCCL groups keep their streams
+    if (!c->ncu) {
+        hipDeviceProp_t prop;
+        HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
+        c->ncu = prop.multiProcessorCount;
+    }
+    const int per_xcd = std::max(1, c->ncu / 8);
+    const double share = (double)band_cols / (double)std::max(1LL, band_cols + (long long)c->sweep_depth * deep_cols);
+    long want = env_long("IBLB_BAND_RESERVE_CUS", (share > 0.05 ? 2 : 1) * per_xcd);
+    if (want < 0 || want >= c->ncu) want = 0;
+    if (want == c->band_reserve) return IBLB_OK;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->band_st) {
+        HIP_TRY(c, hipStreamSynchronize(c->band_st));
+        (void)hipStreamDestroy(c->band_st);
+        c->band_st = nullptr;
+    }
+    hipStream_t compute = nullptr;
+    if (want) {
+        std::vector<uint32_t> deep((size_t)(c->ncu + 31) / 32, 0u), band(deep.size(), 0u);
+        for (int i = 0; i < c->ncu; ++i) {
+            std::vector<uint32_t>& m = i >= c->ncu - want ? band : deep;
+            m[(size_t)i / 32] |= 1u << (i % 32);
+        }
+        HIP_TRY(c, hipExtStreamCreateWithCUMask(&compute, (uint32_t)deep.size(), deep.data()));
+        HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->band_st, (uint32_t)band.size(), band.data()));
+        for (hipEvent_t* e : {&c->ev_b0, &c->ev_b2})
+            if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventDisableSystemFence));
+    } else {
+        HIP_TRY(c, hipStreamCreateWithFlags(&compute, hipStreamNonBlocking));
+    }
+    (void)hipStreamDestroy(c->stream);
+    c->stream = compute;
+    c->band_reserve = (int)want;
+    return IBLB_OK;
+}
+
 // IB band plan of the points s (host copy) for band_step; band_valid stays false where the
 // cycle does not apply (see band_ready) or does not pay (bands over half the lattice, bands
 // within 2(K-1) columns of the lattice edge: the reference's flat-index wrap).
@@ -1200,11 +1278,14 @@ static int plan_bands_t(iblb_ctx* c, int ns, const float* s) {
     if (prev < nx) gaps.push_back({prev, nx});
     long long ndeep = 0;
     for (auto& g : gaps) ndeep += g.second - g.first;
-    // sweeps of ~deep_w columns, balanced to whole rounds of resident waves over the device
+    int rc = band_streams(c, cols, ndeep);
+    if (rc) return rc;
+    // sweeps of ~deep_w columns, balanced to whole rounds of resident waves over the deep
+    // sweep's CUs
     const int W = std::max(1, c->deep_w);
-    int nch = 0, ncu = 0;
+    int nch = 0;
     const int wpc = sweepk_geometry<T>(K, c->deep_vs, c->deep_variant, false, c->ny, &nch);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int ncu = c->ncu - c->band_reserve;
     long nsw = (long)((ndeep + W - 1) / W);
     const long slots = (long)wpc * ncu;
     if (c->deep_balance && slots > 0 && nch > 0 && ndeep > 0) {
@@ -1234,7 +1315,7 @@ static int plan_bands_t(iblb_ctx* c, int ns, const float* s) {
     HIP_TRY(c, hipMemcpy(c->d_band, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
     if (!c->s_alloc) {  // the trapezoid's scratch levels: two buffers laid out like g
         const size_t bytes = (size_t)(2 * c->buf_elems + c->buf_gap + 2 * GUARD) * c->esize;
-        int rc = alloc_zero(c, (void**)&c->s_alloc, bytes);
+        rc = alloc_zero(c, (void**)&c->s_alloc, bytes);
         if (rc) return rc;
         c->sbuf[0] = c->s_alloc + GUARD * c->esize;
         c->sbuf[1] = c->s_alloc + (GUARD + c->buf_elems + c->buf_gap) * c->esize;
