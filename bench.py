@@ -70,6 +70,9 @@ def parse():
     p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                    help="strong (default): the configured lattice over N ranks; weak: N times the "
                         "configured width (K4 weak scaling: (nx*N) x ny, one configured lattice per rank)")
+    p.add_argument("--prime-seconds", type=float, default=1.0,
+                   help="untimed steps before the warmup until this much wall time has passed (the GPU "
+                        "clock settles under load; reported as `prime` in the JSON line)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU sample duration")
     p.add_argument("--no-profile-events", action="store_true", help="skip per-launch HIP events")
@@ -87,8 +90,12 @@ def cpu_baseline(nx, ny, budget_s, points=None):
     workload."""
     from oracle import oracle as O
     from cuda_iblb_11_amd import workloads as W
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
+    node = host_cores()
+    # the host cores this process may use: OMP_NUM_THREADS where the launcher sets it (the GPU
+    # box grants each GPU slot its share of the node, OMP_NUM_THREADS=16 of 128 physical cores),
+    # otherwise every physical core of the node
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or node["physical_cores"] or (os.cpu_count() or 1)
+    threads = max(1, threads)
     kind = "port"
     try:
         O.build(native=True)
@@ -101,7 +108,7 @@ def cpu_baseline(nx, ny, budget_s, points=None):
     ns = 0 if points is None else points[0].size // 2
     est = nx * ny * ns * 2e-8 / threads  # ~20 ns per delta evaluation and core
     if est > 90:
-        return {"value": None, "unit": "MLUPS", "cores": threads, "kind": kind,
+        return {"value": None, "unit": "MLUPS", "cores": threads, "kind": kind, "node": node,
                 "sample": f"skipped: the reference's O(N*Ns) spread needs ~{est:.0f} s per step on {threads} cores"}
     rho, u = W.perturbed_state(nx, ny, W.SEED)
     sim = O.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=W.BODY_FORCE, point_spread=False)
@@ -116,11 +123,37 @@ def cpu_baseline(nx, ny, budget_s, points=None):
     sim.step(n)
     dt = time.perf_counter() - t0
     mlups = nx * ny * n / dt / 1e6
-    return {"value": round(mlups, 3), "unit": "MLUPS", "cores": threads, "kind": kind,
+    return {"value": round(mlups, 3), "unit": "MLUPS", "cores": threads, "kind": kind, "node": node,
             "sample": f"{n} steps of the {nx}x{ny} f64 channel" + (f" + {ns} IB points" if ns else "") +
                       ", reference unfused AoS sequence restated in C "
                       f"(oracle/oracle.c, {'-march=native' if native else 'x86-64-v2'}, OpenMP {threads} threads), "
                       f"{dt:.1f} s"}
+
+
+def host_cores():
+    """Physical cores / sockets / model of the host (lscpu's counts, from /proc/cpuinfo)."""
+    phys, model = set(), ""
+    try:
+        pid = cid = None
+        for ln in open("/proc/cpuinfo"):
+            k, _, v = ln.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "physical id":
+                pid = v
+            elif k == "core id":
+                cid = v
+            elif k == "model name" and not model:
+                model = v
+            elif not k and pid is not None:
+                phys.add((pid, cid))
+                pid = cid = None
+        if pid is not None:
+            phys.add((pid, cid))
+    except OSError:
+        pass
+    return {"physical_cores": len(phys) or None, "sockets": len({p for p, _ in phys}) or None,
+            "logical_cpus": os.cpu_count(), "model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def pmc_valu(workload_key):
@@ -199,6 +232,23 @@ def main():
     if points is not None:
         lat.set_lagrangian(*points)
 
+    # prime: the clock of an idle GPU ramps up over the first ~0.1-1 s of load; a 20-step timed
+    # region (~3 ms at 4096^2) would otherwise measure the ramp (profiles/r02a_bench_*.json: 109k
+    # MLUPS at 20 steps vs 125k at 500 on the same box)
+    # (ranks step together: rank 0's clock decides, broadcast after every chunk)
+    prime_steps, tp = 0, time.perf_counter()
+    while True:
+        go = time.perf_counter() - tp < a.prime_seconds
+        if distributed:
+            flag = torch.tensor([1.0 if go else 0.0], device="cpu" if a.same_device else "cuda")
+            dist.broadcast(flag, src=0)
+            go = bool(flag.item() > 0)
+        if not go:
+            break
+        lat.step(50)
+        lat.synchronize()
+        prime_steps += 50
+    prime_s = time.perf_counter() - tp
     lat.step(a.warmup)
     lat.synchronize()
     # Launch timing for the roofline: HIP events around every collide launch.  At N = 1 without
@@ -349,6 +399,7 @@ def main():
                 "peak": VALU_PEAK_TFLOPS[precision], "unit": "TFLOP/s",
                 "frac": round(valu["flops_per_launch"] / (launch_ms * 1e-3) / 1e12 / VALU_PEAK_TFLOPS[precision], 4),
                 "valu_issue_share": valu.get("valu_issue_share"), "source": valu.get("source")}),
+            "prime": {"steps": prime_steps, "seconds": round(prime_s, 3)},
             "cpu_baseline": cpu,
             "state_finite": finite,
         }

@@ -12,7 +12,8 @@ import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_HERE, "lib", "libiblb.so")
+# IBLB_LIB: another build of the same library (A/B measurements of kernel builds only)
+LIB_PATH = os.environ.get("IBLB_LIB") or os.path.join(_HERE, "lib", "libiblb.so")
 HEADER = os.path.join(REPO, "include", "iblb.h")
 
 IBLB_OK = 0

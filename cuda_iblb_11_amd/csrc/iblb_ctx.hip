@@ -68,6 +68,7 @@ struct iblb_ctx {
     int reserved_cus = 0, ncu = 0;  // CUs kept free of the compute stream (RCCL groups), device CUs
     hipStream_t stream = nullptr;
     Coef coef{};
+    KConst kc{};  // collide constants folded from coef (kernel arguments)
     // populations: two buffers in one allocation (deterministic relative placement of the
     // 18 streams the collide-stream kernel touches), `cur` holds the state
     char* g_alloc = nullptr;
@@ -406,7 +407,7 @@ int launch_boot_step(iblb_ctx* c) {
     T* sr[3];
     send_ptrs<T>(c, sl, sr);
     HIP_TRY(c, launch_boot<T>(gptr<T>(c, c->cur), gptr<T>(c, 1 - c->cur), c->L, c->rho0, c->u0, c->force0, c->fplane,
-                              sl, sr, c->coef, c->stream));
+                              sl, sr, c->coef, c->kc, c->stream));
     return IBLB_OK;
 }
 
@@ -433,6 +434,7 @@ int launch_fused_step(iblb_ctx* c, int col_begin, int ncols, int col_step = 1, b
     a.flux_norm = c->cfg.flux_norm;
     a.Q = c->d_Q;
     a.c = c->coef;
+    a.k = c->kc;
     a.variant = c->variant;
     size_t ev = 0;
     int rc = timed ? ev_begin(c, &ev) : IBLB_OK;
@@ -522,6 +524,7 @@ Sweep2Args<T> sweep_args(iblb_ctx* c, int col_begin, int col_step, int col_end, 
     a.flux_norm = c->cfg.flux_norm;
     a.Q = c->d_Q;
     a.c = c->coef;
+    a.k = c->kc;
     return a;
 }
 
@@ -724,6 +727,7 @@ int band_step(iblb_ctx* c) {
         a.flux_norm = c->cfg.flux_norm;
         a.Q = c->d_Q;
         a.c = c->coef;
+        a.k = c->kc;
         a.variant = c->variant;
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, bs))) return rc;
@@ -1028,6 +1032,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->coef.inv_2cs4 = 1. / (2 * cs * cs * cs * cs);
     c->coef.gx = cfg->body_force[0];
     c->coef.gy = cfg->body_force[1];
+    c->kc = make_kconst(c->coef);
 
     auto bail = [&](int rc) { g_create_error = c->err; iblb_destroy(c); return rc; };
     if (hipSetDevice(c->device) != hipSuccess) return bail(fail(c, IBLB_ERR_HIP, "hipSetDevice failed"));

@@ -199,69 +199,135 @@ __device__ __forceinline__ void moments(const R f[9], R& rho, R& mx, R& my) {
 }
 
 // TRT collision with the reference's Guo forcing (LatticeBoltzmann.cu:30-62, 64-171)
-// written on the even/odd parts of each pair:
+// written on the sum s = f_i + f_ibar and difference d = f_i - f_ibar of each pair
+// (i, ibar) = (1,3) (2,4) (5,7) (6,8):
 //   feq+ = rho w (1 + (c.u)^2/(2cs^4) - u^2/(2cs^2)),   feq- = rho w (c.u)/cs^2
 //   F+   = k w (-(u.F)/cs^2 + (c.u)(c.F)/cs^4),          F-   = k w (c.F)/cs^2
-//   f1_i = f_i - w+ (f+ - feq+) + F+  -  w- (f- - feq-) + F-
-//   f1_ibar = f_ibar - w+ (f+ - feq+) + F+ + w- (f- - feq-) - F-
-//   f1_0 = f_0 - w+ (f_0 - feq_0)                         (no F_0, as in the reference)
-// Algebraically identical to the reference; rounding differs at the 1e-16 level.  The constant
-// products (w+ w, w- w / cs^2, k w, k w / cs^4, k w / cs^2, w+/2, w-/2) are folded per weight
-// class, so a pair costs ~19 fp64 operations instead of ~28 (the multi-iteration kernels are
-// bound by fp64 issue, profiles/r01d5_*):
-//   A = w+ feq+ + F+ - (w+/2)(f_i + f_ibar),   B = w- feq- + F- - (w-/2)(f_i - f_ibar)
-//   f1_i = f_i + (A + B),   f1_ibar = f_ibar + (A - B)
-// DEV: f holds deviations h = f - w and drho = rho - 1 (float storage).
+//   f1_i    = f_i    - w+ (s/2 - feq+) - w- (d/2 - feq-) + F+ + F-
+//   f1_ibar = f_ibar - w+ (s/2 - feq+) + w- (d/2 - feq-) + F+ - F-
+//   f1_0    = f_0 - w+ (f_0 - feq_0)                      (no F_0, as in the reference)
+// With E = w+ feq+ + F+ and O = w- feq- + F-:
+//   f1_i = (1-w+)/2 s + (1-w-)/2 d + (E + O),   f1_ibar = (1-w+)/2 s - (1-w-)/2 d + (E - O)
+// Algebraically identical to the reference; rounding differs at the 1e-16 level.  Every product
+// of constants is folded once on the host (KBase: relaxation / weights; KForce: the force), so
+// a pair costs ~11 operations and the per-cell moments come from the pair sums and
+// differences; the multi-iteration kernels are bound by fp64 issue and register space, and the
+// folded constants are kernel arguments (scalar registers) instead of per-wave recomputations.
+// DEV: f holds deviations h = f - w (float storage); sum = rho - 1.
 __device__ __forceinline__ double fmaR(double a, double b, double c) { return __builtin_fma(a, b, c); }
 __device__ __forceinline__ float fmaR(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
-template <typename R, bool DEV>
-__device__ __forceinline__ void collide(R f[9], R rho, R drho, R ux, R uy, R Fx, R Fy, const Coef& c) {
-#pragma clang fp contract(on)  // fuse within a statement only: the same FMAs in every kernel
-    const R op = (R)c.omega_p, om = (R)c.omega_m;
-    const R a1 = (R)c.inv_2cs2, a2 = (R)c.inv_2cs4, ics2 = (R)c.inv_cs2, ics4 = (R)c.inv_cs4;
-    const R kk = (R)c.kguo;
-    const R usq = ux * ux + uy * uy;
-    const R uF = ux * Fx + uy * Fy;
-    const R base = -usq * a1;              // even equilibrium part common to all i
-    const R ebase = DEV ? base : (R)1 + base;
-    const R guF = -uF * ics2;
-    // rest population: f0 - op (f0 - feq0) = (1 - op) f0 + op feq0
-    {
-        const R w0 = (R)(4. / 9);
-        const R feq0 = DEV ? w0 * (drho + rho * base) : rho * w0 * ebase;
-        f[0] = fmaR((R)1 - op, f[0], op * feq0);
-    }
-    // per weight class (axis w = 1/9, diagonal w = 1/36)
-    R Rp[2], Rm[2], Dp[2], Gc[2];
-#pragma unroll
+// pair p = 0..3: members a(p) (c = (1,0), (0,1), (1,1), (-1,1)) and b(p) = opposite
+__host__ __device__ constexpr int pair_a(int p) { return p == 0 ? 1 : (p == 1 ? 2 : (p == 2 ? 5 : 6)); }
+__host__ __device__ constexpr int pair_b(int p) { return p == 0 ? 3 : (p == 1 ? 4 : (p == 2 ? 7 : 8)); }
+
+// Constants of the collision in the compute type R (weight class cl: 0 = axis 1/9, 1 = diagonal 1/36)
+template <typename R>
+struct KBase {
+    R omp, opw0;           // 1 - w+,  w+ 4/9
+    R opw[2], oqa[2];      // w+ w,    w+ w / (2 cs^4)
+    R omwi2[2];            // w- w / cs^2
+    R kw[2], kwi4[2], kwi2[2];  // k w, k w / cs^4, k w / cs^2   (k = 1 - 1/(2 TAU))
+    R a1, ics2;            // 1/(2 cs^2), 1/cs^2
+    R hs, hd, nhd;         // (1-w+)/2, (1-w-)/2, -(1-w-)/2
+};
+// Force-dependent constants (uniform for a body force; per cell with an IB force)
+template <typename R>
+struct KForce {
+    R Fx, Fy, hFx, hFy;    // F, F/2
+    R hE[4], gO[4];        // per pair: k w (c.F) / cs^4,  k w (c.F) / cs^2
+};
+
+template <typename R>
+__host__ __device__ inline KBase<R> make_kbase(const Coef& c) {
+#pragma clang fp contract(off)
+    KBase<R> b;
+    const R op = (R)c.omega_p, om = (R)c.omega_m, kk = (R)c.kguo;
+    const R ics2 = (R)c.inv_cs2, ics4 = (R)c.inv_cs4, a2 = (R)c.inv_2cs4;
+    b.omp = (R)1 - op;
+    b.opw0 = op * (R)(4. / 9);
     for (int cl = 0; cl < 2; ++cl) {
         const R w = cl == 0 ? (R)(1. / 9) : (R)(1. / 36);
-        Rp[cl] = rho * (op * w);
-        Rm[cl] = rho * (om * w * ics2);
-        Dp[cl] = DEV ? drho * (op * w) : (R)0;
-        Gc[cl] = guF * (kk * w);
+        b.opw[cl] = op * w;
+        b.oqa[cl] = b.opw[cl] * a2;
+        b.omwi2[cl] = om * w * ics2;
+        b.kw[cl] = kk * w;
+        b.kwi4[cl] = b.kw[cl] * ics4;
+        b.kwi2[cl] = b.kw[cl] * ics2;
     }
-    const R hop = (R)0.5 * op, hom = (R)0.5 * om;
+    b.a1 = (R)c.inv_2cs2;
+    b.ics2 = ics2;
+    b.hs = (R)0.5 * b.omp;
+    b.hd = (R)0.5 * ((R)1 - om);
+    b.nhd = -b.hd;
+    return b;
+}
+
+// The same arithmetic on the host (uniform body force) and on the device (per-cell force), so a
+// cell without IB force collides bit-identically in every kernel
+template <typename R>
+__host__ __device__ inline KForce<R> make_kforce(const KBase<R>& b, R Fx, R Fy) {
+#pragma clang fp contract(off)
+    KForce<R> k;
+    k.Fx = Fx;
+    k.Fy = Fy;
+    k.hFx = (R)0.5 * Fx;
+    k.hFy = (R)0.5 * Fy;
+    const R cF[4] = {Fx, Fy, Fx + Fy, Fy - Fx};
+    for (int p = 0; p < 4; ++p) {
+        const int cl = p < 2 ? 0 : 1;
+        k.hE[p] = cF[p] * b.kwi4[cl];
+        k.gO[p] = cF[p] * b.kwi2[cl];
+    }
+    return k;
+}
+
+template <typename R, bool DEV>
+__device__ __forceinline__ void collide_sd(R f[9], const R s[4], const R d[4], R rho, R sum, R ux, R uy,
+                                           const KBase<R>& b, const KForce<R>& k) {
+#pragma clang fp contract(on)  // fuse within a statement only: the same FMAs in every kernel
+    const R usq = ux * ux + uy * uy;
+    const R uF = ux * k.Fx + uy * k.Fy;
+    const R base = -usq * b.a1;            // even equilibrium part common to all i
+    const R ebase = DEV ? base : (R)1 + base;
+    const R guF = -uF * b.ics2;
+    // rest population: f0 - w+ (f0 - feq0) = (1 - w+) f0 + w+ feq0
+    {
+        const R feq0w = DEV ? fmaR(rho, base, sum) * b.opw0 : (rho * ebase) * b.opw0;
+        f[0] = fmaR(b.omp, f[0], feq0w);
+    }
+    // per weight class: E = P + Qa cu^2 + cu hE_p,  O = Rm cu + gO_p
+    R P[2], Qa[2], Rm[2];
+#pragma unroll
+    for (int cl = 0; cl < 2; ++cl) {
+        P[cl] = fmaR(rho * b.opw[cl], ebase, guF * b.kw[cl]);
+        if (DEV) P[cl] = fmaR(sum, b.opw[cl], P[cl]);
+        Qa[cl] = rho * b.oqa[cl];
+        Rm[cl] = rho * b.omwi2[cl];
+    }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-        const int a = p == 0 ? 1 : (p == 1 ? 2 : (p == 2 ? 5 : 6));
-        const int b = p == 0 ? 3 : (p == 1 ? 4 : (p == 2 ? 7 : 8));
+        const int a = pair_a(p), bb = pair_b(p);
         const int cl = p < 2 ? 0 : 1;
-        const R w = cl == 0 ? (R)(1. / 9) : (R)(1. / 36);
         const R cu = (R)cx(a) * ux + (R)cy(a) * uy;
-        const R cF = (R)cx(a) * Fx + (R)cy(a) * Fy;
-        const R P = fmaR(Rp[cl], fmaR(cu * cu, a2, ebase), Dp[cl]);  // w+ feq+
-        const R M = Rm[cl] * cu;                                                        // w- feq-
-        const R Gp = fmaR(cu * cF, kk * w * ics4, Gc[cl]);                     // F+
-        const R Gm = cF * (kk * w * ics2);                                              // F-
-        const R s = f[a] + f[b];
-        const R d = f[a] - f[b];
-        const R A = fmaR(-hop, s, P + Gp);
-        const R B = fmaR(-hom, d, M + Gm);
-        f[a] = f[a] + (A + B);
-        f[b] = f[b] + (A - B);
+        const R E = fmaR(Qa[cl], cu * cu, fmaR(cu, k.hE[p], P[cl]));
+        const R O = fmaR(Rm[cl], cu, k.gO[p]);
+        f[a] = fmaR(s[p], b.hs, fmaR(d[p], b.hd, E + O));
+        f[bb] = fmaR(s[p], b.hs, fmaR(d[p], b.nhd, E - O));
     }
+}
+
+// The collision given rho and u explicitly (boot step)
+template <typename R, bool DEV>
+__device__ __forceinline__ void collide(R f[9], R rho, R drho, R ux, R uy, const KBase<R>& b, const KForce<R>& k) {
+#pragma clang fp contract(on)
+    R s[4], d[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        s[p] = f[pair_a(p)] + f[pair_b(p)];
+        d[p] = f[pair_a(p)] - f[pair_b(p)];
+    }
+    collide_sd<R, DEV>(f, s, d, rho, drho, ux, uy, b, k);
 }
 
 // 1/x: v_rcp (about single precision) refined by two Newton steps (within an ulp of the
@@ -276,25 +342,60 @@ __device__ __forceinline__ float recip(float x) {
     return __builtin_fmaf(r, __builtin_fmaf(-x, r, 1.f), r);
 }
 
-// One cell of a collide-stream step: f = the pulled populations f^t (deviations if DEV),
-// force = body force + IB force of this cell (double).  rho and u^t = (sum c f + force/2)/rho
+// One cell of a collide-stream step: f = the pulled populations f^t (deviations if DEV), k = the
+// constants of the cell's force (body force + IB force).  rho and u^t = (sum c f + F/2)/rho
 // (ImmersedBoundary.cu:249-255) from f, then collide in place; returns u_x (flux sample).
 // Contraction is per statement (fp contract(on)), not left to the backend, so the one-step and
-// the multi-iteration kernels round every cell identically whatever code surrounds them.
+// the multi-iteration kernels round every cell identically whatever code surrounds them.  The
+// moments come from the pair sums / differences the collision needs anyway:
+// rho = f0 + s13 + s24 + s57 + s68, m_x = d13 + d57 - d68, m_y = d24 + d57 + d68.
 template <typename R, bool DEV>
-__device__ __forceinline__ R relax_cell(R f[9], double fx, double fy, const Coef& c) {
+__device__ __forceinline__ R relax_cell(R f[9], const KBase<R>& b, const KForce<R>& k) {
 #pragma clang fp contract(on)
-    R s, mx, my;
-    moments<R>(f, s, mx, my);
-    const R rho = DEV ? (R)1 + s : s;
-    const R Fx = (R)fx;
-    const R Fy = (R)fy;
+    R s[4], d[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        s[p] = f[pair_a(p)] + f[pair_b(p)];
+        d[p] = f[pair_a(p)] - f[pair_b(p)];
+    }
+    const R sum = f[0] + ((s[0] + s[1]) + (s[2] + s[3]));
+    const R mx = d[0] + (d[2] - d[3]);
+    const R my = d[1] + (d[2] + d[3]);
+    const R rho = DEV ? (R)1 + sum : sum;
     const R inv = recip(rho);
-    const R ux = (mx + (R)0.5 * Fx) * inv;
-    const R uy = (my + (R)0.5 * Fy) * inv;
-    collide<R, DEV>(f, rho, s, ux, uy, Fx, Fy, c);
+    const R ux = (mx + k.hFx) * inv;
+    const R uy = (my + k.hFy) * inv;
+    collide_sd<R, DEV>(f, s, d, rho, sum, ux, uy, b, k);
     return ux;
 }
+
+// Collide constants of both compute types, folded once on the host (kernel arguments)
+struct KConst {
+    KBase<double> bd;
+    KBase<float> bf;
+    KForce<double> fd;  // the uniform body force
+    KForce<float> ff;
+};
+inline KConst make_kconst(const Coef& c) {
+    KConst k;
+    k.bd = make_kbase<double>(c);
+    k.bf = make_kbase<float>(c);
+    k.fd = make_kforce<double>(k.bd, c.gx, c.gy);
+    k.ff = make_kforce<float>(k.bf, (float)c.gx, (float)c.gy);
+    return k;
+}
+template <typename R>
+__host__ __device__ inline const KBase<R>& kbase(const KConst& k);
+template <>
+__host__ __device__ inline const KBase<double>& kbase<double>(const KConst& k) { return k.bd; }
+template <>
+__host__ __device__ inline const KBase<float>& kbase<float>(const KConst& k) { return k.bf; }
+template <typename R>
+__host__ __device__ inline const KForce<R>& kbody(const KConst& k);
+template <>
+__host__ __device__ inline const KForce<double>& kbody<double>(const KConst& k) { return k.fd; }
+template <>
+__host__ __device__ inline const KForce<float>& kbody<float>(const KConst& k) { return k.ff; }
 
 // ImmersedBoundary.cu:21-81, with the reference's float/double rounding points.
 // Compiled with contraction off so it matches the C restatement bit for bit.

@@ -34,6 +34,7 @@ struct FusedArgs {
     double flux_norm;
     double* Q;
     Coef c;
+    KConst k;           // collide constants folded on the host (iblb_device.h)
     int variant;        // kernel variant (MODE bits of lbm_kernels.hip), 0 = default
 };
 
@@ -85,6 +86,7 @@ struct Sweep2Args {
     double flux_norm;
     double* Q;
     Coef c;
+    KConst k;            // collide constants folded on the host (iblb_device.h)
 };
 
 // slab: true = the group kernel (halo columns from recv_*, send buffers written); false = lone
@@ -116,7 +118,7 @@ hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s);
 template <typename T>
 hipError_t launch_boot(const T* src, T* dst, Layout L, const double* rho0, const double* u0,
                        const double* force0, long fplane, T* const send_left[3], T* const send_right[3],
-                       Coef c, hipStream_t s);
+                       Coef c, KConst k, hipStream_t s);
 
 // Macroscopic output in the reference layout (slab-local j = y*ncol + xc):
 // rho = sum f, u = (sum c f + force/2)/rho with force = g + dense IB force.

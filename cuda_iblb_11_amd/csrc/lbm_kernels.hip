@@ -88,7 +88,10 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
 #pragma unroll
     for (int e = 0; e < V; ++e) {
         R f[9] = {(R)v0[e], (R)v1[e], (R)v2[e], (R)v3[e], (R)v4[e], (R)v5[e], (R)v6[e], (R)v7[e], (R)v8[e]};
-        const R ux = relax_cell<R, DEV>(f, a.c.gx + fxv[e], a.c.gy + fyv[e], a.c);
+        const KBase<R>& kb = kbase<R>(a.k);
+        // body force only: the host-folded constants; with an IB force: the same fold per cell
+        const R ux = (IB && has_f) ? relax_cell<R, DEV>(f, kb, make_kforce<R>(kb, (R)(a.c.gx + fxv[e]), (R)(a.c.gy + fyv[e])))
+                                   : relax_cell<R, DEV>(f, kb, kbody<R>(a.k));
         if (do_flux && y0 + e < L.ny) q += (double)ux / a.flux_norm;
         v0[e] = (T)f[0]; v1[e] = (T)f[1]; v2[e] = (T)f[2]; v3[e] = (T)f[3]; v4[e] = (T)f[4];
         v5[e] = (T)f[5]; v6[e] = (T)f[6]; v7[e] = (T)f[7]; v8[e] = (T)f[8];
@@ -151,7 +154,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void boot_kernel(const T* __restrict__ src, T* __restrict__ dst, Layout L,
                                                    const double* __restrict__ rho0, const double* __restrict__ u0,
                                                    const double* __restrict__ force0, long fplane, SendPtrs<T> sp,
-                                                   Coef c) {
+                                                   Coef c, KConst kc) {
     typedef typename Calc<T>::R R;
     constexpr bool DEV = Store<T>::dev;
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -164,7 +167,8 @@ __global__ __launch_bounds__(256) void boot_kernel(const T* __restrict__ src, T*
     const double rho = rho0[of];
     const R ux = (R)u0[of], uy = (R)u0[fplane + of];
     const R Fx = (R)(c.gx + (force0 ? force0[of] : 0.)), Fy = (R)(c.gy + (force0 ? force0[fplane + of] : 0.));
-    collide<R, DEV>(f, (R)rho, (R)(rho - 1.0), ux, uy, Fx, Fy, c);
+    const KBase<R>& kb = kbase<R>(kc);
+    collide<R, DEV>(f, (R)rho, (R)(rho - 1.0), ux, uy, kb, make_kforce<R>(kb, Fx, Fy));
 #pragma unroll
     for (int i = 0; i < 9; ++i) dst[i * L.plane + o] = (T)f[i];
     if (xc == 0 && sp.left[0]) { sp.left[0][y] = (T)f[3]; sp.left[1][y] = (T)f[6]; sp.left[2][y] = (T)f[7]; }
@@ -173,11 +177,11 @@ __global__ __launch_bounds__(256) void boot_kernel(const T* __restrict__ src, T*
 
 template <typename T>
 hipError_t launch_boot(const T* src, T* dst, Layout L, const double* rho0, const double* u0, const double* force0,
-                       long fplane, T* const send_left[3], T* const send_right[3], Coef c, hipStream_t s) {
+                       long fplane, T* const send_left[3], T* const send_right[3], Coef c, KConst k, hipStream_t s) {
     SendPtrs<T> sp;
     for (int p = 0; p < 3; ++p) { sp.left[p] = send_left[p]; sp.right[p] = send_right[p]; }
     const long n = (long)L.ncol * L.ny;
-    boot_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(src, dst, L, rho0, u0, force0, fplane, sp, c);
+    boot_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(src, dst, L, rho0, u0, force0, fplane, sp, c, k);
     return hipGetLastError();
 }
 
@@ -322,7 +326,7 @@ hipError_t launch_field_out(const double* lay, double* ref, Layout L, int ncomp,
 #define IBLB_INST(T)                                                                                            \
     template hipError_t launch_fused<T>(const FusedArgs<T>&, hipStream_t);                                      \
     template hipError_t launch_boot<T>(const T*, T*, Layout, const double*, const double*, const double*, long,  \
-                                       T* const[3], T* const[3], Coef, hipStream_t);                            \
+                                       T* const[3], T* const[3], Coef, KConst, hipStream_t);                            \
     template hipError_t launch_macro_out<T>(const T*, Layout, Halo<T>, const double*, long, double, double,      \
                                             double*, double*, hipStream_t);                                     \
     template hipError_t launch_pop_out<T>(const T*, Layout, Halo<T>, double*, int, hipStream_t);                     \

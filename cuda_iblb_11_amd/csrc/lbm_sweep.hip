@@ -150,7 +150,7 @@ __device__ __forceinline__ void load_raw(const Sweep2Args<T>& a, int x, int row0
 template <typename T, int VS>
 __device__ __forceinline__ void pull_window(const T (*pk[9])[VS], const T* edge, const T (&m2)[VS], const T (&m4)[VS],
                                             T m7, T m8, const T (&m5)[VS], const T (&m6)[VS], int lane, int r0,
-                                            int et, T s[9][VS]) {
+                                            int et, T s[9][VS], bool walls = true) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
         if (cy(k) == 0) {
@@ -162,6 +162,7 @@ __device__ __forceinline__ void pull_window(const T (*pk[9])[VS], const T* edge,
             shift_rows<T, VS, -1>(*pk[k], edge ? edge + k : nullptr, lane, s[k]);
         }
     }
+    if (!walls) return;  // wave-uniform: the wave holds neither wall row
     if (r0 == 0) {  // bounce-back on y = 0 (LatticeBoltzmann.cu:328-340)
         s[2][0] = m4[0];
         s[5][0] = m7;
@@ -187,7 +188,6 @@ __device__ __forceinline__ double sweep_walk(const Sweep2Args<T>& a, int xa, int
     typedef typename Calc<T>::R R;
     constexpr bool DEV = Store<T>::dev;
     const Layout L = a.L;
-    const double gx = a.c.gx, gy = a.c.gy;
     // first, last and next column of the walk
     const int x0 = REV ? xb : xa - 1, x1 = REV ? xa - 1 : xb, dx = REV ? -1 : 1;
 
@@ -229,7 +229,7 @@ __device__ __forceinline__ double sweep_walk(const Sweep2Args<T>& a, int xa, int
                 R f[9];
 #pragma unroll
                 for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
-                const R ux = relax_cell<R, DEV>(f, gx, gy, a.c);
+                const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
                 if (flux1 && owner && r0 + e < L.ny) q += (double)ux / a.flux_norm;
 #pragma unroll
                 for (int k = 0; k < 9; ++k) C[k][e] = (T)f[k];
@@ -251,7 +251,7 @@ __device__ __forceinline__ double sweep_walk(const Sweep2Args<T>& a, int xa, int
                 R f[9];
 #pragma unroll
                 for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
-                const R ux = relax_cell<R, DEV>(f, gx, gy, a.c);
+                const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
                 if (flux2 && owner && r0 + e < L.ny) q += (double)ux / a.flux_norm;
 #pragma unroll
                 for (int k = 0; k < 9; ++k) s[k][e] = (T)f[k];
@@ -398,10 +398,11 @@ hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s) {
 // arithmetic is fused_kernel's (relax_cell): bit-identical to K one-step launches.
 //
 // Software-pipelined walk over the level-1 columns xa-(K-1) .. xb+(K-2) (dx = +1, or -1 from
-// the right end): iteration i issues the loads of g^t column x, computes level l >= 2 of column
-// x - l*dx (level 2 from level-1 columns of earlier iterations, level l > 2 from level l-1's
-// window and the column level l-1 made in this iteration), then level 1 of column x.  The loads
-// fly while K-1 levels of arithmetic run, without a second register set for a prefetched column.
+// the right end): iteration i makes level 1 of column x from the rows loaded in the previous
+// iteration, issues the loads of column x + dx, then makes level l = 2 .. K of column
+// x - (l-1)*dx from level l-1's window.  The loads fly while K-1 levels of arithmetic run, and
+// every level (level 1 included) keeps only its two previous columns between iterations.
+// Wall rows (y = 0, Y-1) are patched only by the waves that hold them (a wave-uniform branch).
 //
 // Algorithmic HBM bytes per launch: one read + one write of the state (144 B per cell in f64)
 // for K lattice updates, plus the edge re-reads of neighbouring sweeps (served by L2 under the
@@ -451,21 +452,47 @@ __device__ __forceinline__ void load_raw_periodic(const Sweep2Args<T>& a, int x,
 // walking direction DX): the output is B's column; flux: add u_x of the owned rows to q
 template <typename T, int VS, int DX>
 __device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (&B)[9][VS], const T (&C)[9][VS],
-                                                  const Sweep2Args<T>& a, int lane, int r0, int et, bool flux,
-                                                  bool owner, double& q, T (&out)[9][VS]) {
+                                                  const Sweep2Args<T>& a, int lane, int r0, int et, bool walls,
+                                                  bool flux, bool owner, double& q, T (&out)[9][VS]) {
     typedef typename Calc<T>::R R;
     constexpr bool DEV = Store<T>::dev;
     const T(*pk[9])[VS];
 #pragma unroll
     for (int k = 0; k < 9; ++k) pk[k] = cx(k) == DX ? &A[k] : (cx(k) == -DX ? &C[k] : &B[k]);
     T s[9][VS];
-    pull_window<T, VS>(pk, nullptr, B[2], B[4], B[7][0], B[8][0], B[5], B[6], lane, r0, et, s);
+    pull_window<T, VS>(pk, nullptr, B[2], B[4], B[7][0], B[8][0], B[5], B[6], lane, r0, et, s, walls);
 #pragma unroll
     for (int e = 0; e < VS; ++e) {
         R f[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
-        const R ux = relax_cell<R, DEV>(f, a.c.gx, a.c.gy, a.c);
+        const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
+        if (flux && owner && r0 + e < a.L.ny) q += (double)ux / a.flux_norm;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) out[k][e] = (T)f[k];
+    }
+}
+
+// level 1 of one column from its loaded g^t rows
+template <typename T, int VS>
+__device__ __forceinline__ void level_from_raw(const Raw<T, VS>& cur, const Sweep2Args<T>& a, int lane, int r0, int et,
+                                               bool walls, bool flux, bool owner, double& q, T (&out)[9][VS]) {
+    typedef typename Calc<T>::R R;
+    constexpr bool DEV = Store<T>::dev;
+    const T(*pk[9])[VS];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) pk[k] = &cur.v[k];
+    T s[9][VS];
+    T t5[VS], t6[VS];
+#pragma unroll
+    for (int e = 0; e < VS; ++e) { t5[e] = cur.w[2]; t6[e] = cur.w[3]; }
+    pull_window<T, VS>(pk, cur.e, cur.v[2], cur.v[4], cur.w[0], cur.w[1], t5, t6, lane, r0, et, s, walls);
+#pragma unroll
+    for (int e = 0; e < VS; ++e) {
+        R f[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
+        const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
         if (flux && owner && r0 + e < a.L.ny) q += (double)ux / a.flux_norm;
 #pragma unroll
         for (int k = 0; k < 9; ++k) out[k][e] = (T)f[k];
@@ -480,85 +507,63 @@ __device__ __forceinline__ void copy_col(T (&d)[9][VS], const T (&s)[9][VS]) {
         for (int e = 0; e < VS; ++e) d[k][e] = s[k][e];
 }
 
+// Iteration i of the walk (column x = x0 + i*dx): level 1 of x from the rows loaded in the
+// previous iteration, then the loads of column x + dx (they fly during the remaining levels),
+// then level l = 2 .. K of column x - (l-1)*dx from level l-1's window: WA / WB = its columns
+// made two and one iterations ago, and N = the one made in this iteration.  Level l starts at
+// iteration 2(l-1), when its window holds three valid columns; its columns in [xa, xb) (stored at
+// level K, counted in the flux) all come later.  (Running every level from iteration 0 instead,
+// on not-yet-valid windows, lets the compiler hoist the collide constants out of the walk and
+// needs more registers than the wave has: measured 40 % slower, profiles/r02c_*.)
+template <typename T, int VS, int MODE, int K, bool SLAB, bool REV>
+__device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int nl1, int x0, int xa, int xb, int row0,
+                                            unsigned off, int lane, int r0, int et, bool owner, bool bot, bool top,
+                                            bool walls, T (&WA)[K - 1][9][VS], T (&WB)[K - 1][9][VS],
+                                            Raw<T, VS>& cur, double& q) {
+    constexpr int DX = REV ? -1 : 1;
+    const int x = x0 + i * DX;
+    T N[9][VS];
+    level_from_raw<T, VS>(cur, a, lane, r0, et, walls, x == a.flux_col && x >= xa && x < xb, owner, q, N);
+    if (i + 1 < nl1) load_raw_periodic<T, VS, MODE, SLAB, K>(a, x + DX, row0, off, bot, top, cur);
+#pragma unroll
+    for (int l = 2; l <= K; ++l) {
+        const int c = x - (l - 1) * DX;
+        const bool mine = c >= xa && c < xb;  // implies made (see above)
+        const bool flux = mine && c == a.flux_col;
+        T out[9][VS];
+        const bool made = i >= 2 * (l - 1);
+        if (made) level_from_window<T, VS, DX>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, owner, q, out);
+        if (made && l == K && mine && owner) {
+            T* dst = a.dst + (long)c * a.L.col + row0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * a.L.plane, off, out[k]);
+        }
+        copy_col<T, VS>(WA[l - 2], WB[l - 2]);
+        copy_col<T, VS>(WB[l - 2], N);
+        if (l < K && made) copy_col<T, VS>(N, out);
+    }
+}
+
+// The walk over the level-1 columns.  (Unrolling it by two or three so that the window columns
+// are renamed instead of copied measured 10-20 % slower: more live registers, profiles/r02d_*.)
 template <typename T, int VS, int MODE, int K, bool SLAB, bool REV>
 __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
-                                              int lane, int r0, int et, bool owner, bool bot, bool top) {
-    typedef typename Calc<T>::R R;
-    constexpr bool DEV = Store<T>::dev;
-    constexpr int DX = REV ? -1 : 1;
-    const Layout L = a.L;
+                                              int lane, int r0, int et, bool owner, bool bot, bool top, bool walls) {
     const int x0 = REV ? xb + K - 2 : xa - (K - 1);
     const int nl1 = xb - xa + 2 * (K - 1);  // level-1 columns xa-(K-1) .. xb+(K-2)
-    // level 1: A1 = g1[x-3dx], B1 = g1[x-2dx], C1 = g1[x-dx]; level l in 2..K-1: WA[l-2] and
-    // WB[l-2] = its columns x-(l+2)dx and x-(l+1)dx (the newest one is made in the iteration)
-    T A1[9][VS], B1[9][VS], C1[9][VS];
-    T WA[K - 2][9][VS], WB[K - 2][9][VS];
+    T WA[K - 1][9][VS], WB[K - 1][9][VS];
 #pragma unroll
-    for (int k = 0; k < 9; ++k)
+    for (int l = 0; l < K - 1; ++l)
 #pragma unroll
-        for (int e = 0; e < VS; ++e) {
-            A1[k][e] = B1[k][e] = C1[k][e] = (T)0;
+        for (int k = 0; k < 9; ++k)
 #pragma unroll
-            for (int l = 0; l < K - 2; ++l) WA[l][k][e] = WB[l][k][e] = (T)0;
-        }
+            for (int e = 0; e < VS; ++e) WA[l][k][e] = WB[l][k][e] = (T)0;
     double q = 0.;
-    for (int i = 0; i <= nl1; ++i) {
-        const int x = x0 + i * DX;
-        const bool l1 = i < nl1;
-        Raw<T, VS> cur;
-        if (l1) load_raw_periodic<T, VS, MODE, SLAB, K>(a, x, row0, off, bot, top, cur);
-
-        // ---- levels 2 .. K of columns x - l*dx ----
-        T N[9][VS];  // the column the previous level made in this iteration
-#pragma unroll
-        for (int l = 2; l <= K; ++l) {
-            T out[9][VS];
-            const bool made = i >= 2 * l - 1;
-            if (made) {
-                const int c = x - l * DX;
-                const bool flux = c == a.flux_col && c >= xa && c < xb;
-                if (l == 2) level_from_window<T, VS, DX>(A1, B1, C1, a, lane, r0, et, flux, owner, q, out);
-                else level_from_window<T, VS, DX>(WA[l - 3], WB[l - 3], N, a, lane, r0, et, flux, owner, q, out);
-                if (l == K && owner) {
-                    T* dst = a.dst + (long)c * L.col + row0;
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * L.plane, off, out[k]);
-                }
-            }
-            // level l-1 (>= 2) made N in this iteration: rotate its window
-            if (l >= 3 && i >= 2 * (l - 1) - 1) {
-                copy_col<T, VS>(WA[l - 3], WB[l - 3]);
-                copy_col<T, VS>(WB[l - 3], N);
-            }
-            if (made && l < K) copy_col<T, VS>(N, out);
-        }
-        // ---- level 1 of column x from the loads ----
-        T N1[9][VS];
-        if (l1) {
-            const T(*pk[9])[VS];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) pk[k] = &cur.v[k];
-            T s[9][VS];
-            T t5[VS], t6[VS];
-#pragma unroll
-            for (int e = 0; e < VS; ++e) { t5[e] = cur.w[2]; t6[e] = cur.w[3]; }
-            pull_window<T, VS>(pk, cur.e, cur.v[2], cur.v[4], cur.w[0], cur.w[1], t5, t6, lane, r0, et, s);
-            const bool flux1 = x == a.flux_col && x >= xa && x < xb;
-#pragma unroll
-            for (int e = 0; e < VS; ++e) {
-                R f[9];
-#pragma unroll
-                for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
-                const R ux = relax_cell<R, DEV>(f, a.c.gx, a.c.gy, a.c);
-                if (flux1 && owner && r0 + e < L.ny) q += (double)ux / a.flux_norm;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) N1[k][e] = (T)f[k];
-            }
-        }
-        copy_col<T, VS>(A1, B1);
-        copy_col<T, VS>(B1, C1);
-        if (l1) copy_col<T, VS>(C1, N1);
-    }
+    Raw<T, VS> cur;
+    load_raw_periodic<T, VS, MODE, SLAB, K>(a, x0, row0, off, bot, top, cur);
+    for (int i = 0; i < nl1; ++i)
+        sweepk_iter<T, VS, MODE, K, SLAB, REV>(a, i, nl1, x0, xa, xb, row0, off, lane, r0, et, owner, bot, top, walls, WA,
+                                               WB, cur, q);
     return q;
 }
 
@@ -610,10 +615,12 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     const bool owner = lane >= G && lane < 64 - G && r0 < a.L.ny;
     const bool bot = r0 == 0;
     const bool top = et >= 0 && et < VS;
-    const double q = (a.alt && (sw & 1))
-                         ? sweepk_walk<T, VS, MODE, K, SLAB, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
-                         : sweepk_walk<T, VS, MODE, K, SLAB, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot,
-                                                                     top);
+    // wave-uniform: does the wave hold a wall row (y = 0 or Y-1, ghost lanes included)?
+    const bool walls = row0 <= 0 || row0 + 64 * VS >= a.L.ny;
+    const double q =
+        (a.alt && (sw & 1))
+            ? sweepk_walk<T, VS, MODE, K, SLAB, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top, walls)
+            : sweepk_walk<T, VS, MODE, K, SLAB, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top, walls);
     if (a.flux_col >= xa && a.flux_col < xb) {
         const double qs = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, qs);

@@ -59,9 +59,11 @@ __device__ __forceinline__ void st_plane(T* p, typename VT<T, V>::type v) {
 
 // Move a 32/64-bit value one lane up (dir = +1: lane l receives lane l-1) or down
 // (dir = -1: lane l receives lane l+1) across the whole wave with DPP.
+// bound_ctrl: the lane without a source (lane 0 / lane 63) reads 0, so no register has to be
+// initialised with an "old" value first (one v_mov_b32 less per shifted dword)
 template <int DIR>
 __device__ __forceinline__ int dpp_shift(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, DIR > 0 ? 0x138 : 0x130, 0xf, 0xf, false);
+    return __builtin_amdgcn_mov_dpp(v, DIR > 0 ? 0x138 : 0x130, 0xf, 0xf, true);
 }
 template <int DIR>
 __device__ __forceinline__ double lane_shift(double v) {
