@@ -95,6 +95,7 @@ _SIGS = {
     "iblb_device_count": ([C.POINTER(C.c_int)], C.c_int),
     "iblb_set_state": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
     "iblb_set_lagrangian": ([_vp, C.c_int, _vp, _vp, _vp], C.c_int),
+    "iblb_set_lagrangian_steps": ([_vp, C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
     "iblb_set_cilia": ([_vp, C.POINTER(Cilia)], C.c_int),
     "iblb_get_lagrangian": ([_vp, _vp, _vp, _vp], C.c_int),
     "iblb_step": ([_vp, C.c_int], C.c_int),

@@ -97,6 +97,22 @@ struct iblb_ctx {
     float* d_Fs = nullptr;
     int* d_eps = nullptr;
     float* d_Fs_sum = nullptr;  // F_s summed over an RCCL group (reader scratch)
+    // points given ahead (iblb_set_lagrangian_steps): entry i is used by iteration sch_t0 + i;
+    // d_s / d_us / d_eps hold the entry of the current iteration (sch_cur)
+    float* d_sch_s = nullptr;
+    float* d_sch_us = nullptr;
+    int* d_sch_eps = nullptr;
+    size_t sch_cap = 0;  // entries allocated
+    int sch_n = 0, sch_cur = -1;
+    long long sch_t0 = 0;
+    // band plans of a schedule: one per cycle from the x coordinates of the cycle's entries
+    // (host copies), installed when the cycle's bands differ from the installed ones
+    std::vector<float> sch_x;       // [sch_n][ns]
+    std::vector<float> sch_x_prev;  // the points before the schedule (their force may be owed)
+    std::vector<std::pair<int, int>> band_b;  // merged forced intervals of the installed plan
+    std::vector<int> band_host[2];            // host staging of the uploaded tables (alternating)
+    int band_host_i = 0;
+    bool band_sticky = false;                 // keep the reserved XCDs while a schedule runs
     double* fdense = nullptr;
     uint8_t* flags = nullptr;
     // IB bands of the K-iteration cycle (lone slab, points fixed between iblb_set_lagrangian
@@ -116,8 +132,9 @@ struct iblb_ctx {
     // the band chain beside the deep sweep: CUs reserved for it (whole XCDs, IBLB_BAND_RESERVE_CUS;
     // 0 = both on the compute stream, in sequence)
     int band_reserve = 0;
-    hipStream_t band_st = nullptr;
-    hipEvent_t ev_b0 = nullptr, ev_b2 = nullptr;
+    hipStream_t band_st = nullptr;   // the band chain (masked to the reserved CUs)
+    hipStream_t deep_st = nullptr;   // the cycle's deep sweep (masked to the other CUs)
+    hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_b2 = nullptr;
     // flux: d_Q[0] cumulative, d_Q[1] scratch
     double* d_Q = nullptr;
     // state machine
@@ -190,6 +207,28 @@ bool single_slab(const iblb_ctx* c) {
 }
 bool rccl_multi(const iblb_ctx* c) { return c->transport == TR_RCCL && (c->nranks > 1 || c->self_ring); }
 bool ib_active(const iblb_ctx* c) { return c->max_points > 0 && c->ns > 0; }
+
+// schedule entry of iteration it (clamped to the last one)
+int sched_entry(const iblb_ctx* c, long long it) {
+    const long long e = it - c->sch_t0;
+    return (int)std::max(0LL, std::min(e, (long long)c->sch_n - 1));
+}
+template <typename P>
+P* sched_ptr(P* base, const iblb_ctx* c, int e, int per_point) { return base + (size_t)e * per_point * c->ns; }
+
+// the current points become those of schedule entry e (copies on the context's stream)
+int sched_use(iblb_ctx* c, int e) {
+    if (c->sch_n <= 0 || e == c->sch_cur) return IBLB_OK;
+    const size_t ns = (size_t)c->ns;
+    HIP_TRY(c, hipMemcpyAsync(c->d_s, sched_ptr(c->d_sch_s, c, e, 2), 2 * ns * sizeof(float), hipMemcpyDeviceToDevice,
+                              c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_us, sched_ptr(c->d_sch_us, c, e, 2), 2 * ns * sizeof(float),
+                              hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_eps, sched_ptr(c->d_sch_eps, c, e, 1), ns * sizeof(int), hipMemcpyDeviceToDevice,
+                              c->stream));
+    c->sch_cur = e;
+    return IBLB_OK;
+}
 
 // periodic images of a lone slab: the edge columns of the buffer g itself
 template <typename T>
@@ -267,6 +306,7 @@ int ev_end(iblb_ctx* c, size_t idx, int kind, long long cells = 0, hipStream_t s
         HIP_TRY(c, hipEventSynchronize(c->ev_pool[idx + 1]));
         if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));
         if (c->band_st) HIP_TRY(c, hipStreamSynchronize(c->band_st));
+        if (c->deep_st) HIP_TRY(c, hipStreamSynchronize(c->deep_st));
         for (auto& r : c->ev_kind) {
             float ms = 0.f;
             HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_pool[r.idx], c->ev_pool[r.idx + 1]));
@@ -667,15 +707,16 @@ int band_step(iblb_ctx* c) {
     const T* A = gptr<T>(c, c->cur);
     T* B = gptr<T>(c, 1 - c->cur);
     T* S[2] = {(T*)c->sbuf[0], (T*)c->sbuf[1]};
-    // overlapped: the deep sweep on the compute stream (masked to the CUs outside the reserved
-    // XCDs), the band chain on band_st (the reserved XCDs).  The chain starts with the compute
-    // stream's work so far (deep sweep of the previous cycle included); the compute stream waits
-    // for the chain at the end of the cycle, after the deep sweep is queued.
+    // overlapped: the deep sweep on deep_st (masked to the CUs outside the reserved XCDs), the
+    // band chain on band_st (the reserved XCDs).  The context's own stream keeps the whole chip
+    // (iblb_get_stream hands it out; every other step runs on it): the two masked streams start
+    // after its work so far, and it waits for both at the end of the cycle.
     const bool ov = c->band_st != nullptr;
-    hipStream_t bs = ov ? c->band_st : c->stream, ds = c->stream;
+    hipStream_t bs = ov ? c->band_st : c->stream, ds = ov ? c->deep_st : c->stream;
     if (ov) {
         HIP_TRY(c, hipEventRecord(c->ev_b0, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_b0, 0));
+        HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_b0, 0));
     }
     if (c->ib_state == IB_PENDING) {  // force^t from g^t
         size_t ev = 0;
@@ -703,10 +744,19 @@ int band_step(iblb_ctx* c) {
         const T* src = j == 0 ? A : S[(j - 1) & 1];
         T* dst = j == K - 1 ? B : S[j & 1];
         if (j > 0) {  // force^{t+j} from the level below (valid on the band +- (K-j) columns)
+            // with the points of iteration t+j-1 (a schedule given ahead, or the static points)
+            const float *ps = c->d_s, *pus = c->d_us;
+            const int* pe = c->d_eps;
+            if (c->sch_n > 0) {
+                const int e = sched_entry(c, c->t + j - 1);
+                ps = sched_ptr(c->d_sch_s, c, e, 2);
+                pus = sched_ptr(c->d_sch_us, c, e, 2);
+                pe = sched_ptr(c->d_sch_eps, c, e, 1);
+            }
             size_t ev = 0;
             if ((rc = ev_begin(c, &ev, bs))) return rc;
-            HIP_TRY(c, launch_ib_point<T>(src, c->L, halo_at<T>(c, src), c->nx, c->ns, c->d_s, c->d_us, c->d_eps,
-                                          c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, bs));
+            HIP_TRY(c, launch_ib_point<T>(src, c->L, halo_at<T>(c, src), c->nx, c->ns, ps, pus, pe, c->d_Fs, c->fdense,
+                                          c->fplane, c->flags, c->nch, 64 * c->V, bs));
             if ((rc = ev_end(c, ev, EV_IB, 0, bs))) return rc;
         }
         FusedArgs<T> a;
@@ -735,14 +785,17 @@ int band_step(iblb_ctx* c) {
         if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * c->ny, bs))) return rc;
     }
     if (ov) {
+        HIP_TRY(c, hipEventRecord(c->ev_b1, ds));
         HIP_TRY(c, hipEventRecord(c->ev_b2, bs));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b1, 0));
         HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b2, 0));
     }
     c->cur = 1 - c->cur;
     c->t += K;
     c->halo_valid = false;
     c->ib_state = IB_PENDING;
-    return IBLB_OK;
+    // the force now owed is that of iteration t+K-1's points
+    return c->sch_n > 0 ? sched_use(c, sched_entry(c, c->t - 1)) : IBLB_OK;
 }
 
 template <typename T>
@@ -857,6 +910,13 @@ int step_one(iblb_ctx* c) {
             if ((rc = ensure_force(c))) return rc;
         }
         if ((rc = run_cilia(c))) return rc;
+    } else if (c->sch_n > 0 && sched_entry(c, c->t) != c->sch_cur) {
+        // the force owed to the previous iteration's points first, then this iteration's points
+        if (c->phase == PH_RUN) {
+            if ((rc = ensure_halo(c))) return rc;
+            if ((rc = ensure_force(c))) return rc;
+        }
+        if ((rc = sched_use(c, sched_entry(c, c->t)))) return rc;
     }
     if (c->phase == PH_RUN && rccl_multi(c) && c->overlap && !c->halo_valid && c->ib_state != IB_PENDING &&
         c->ncol >= 3)
@@ -1111,11 +1171,12 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
-    if (c->band_st) {
-        (void)hipStreamSynchronize(c->band_st);
-        (void)hipStreamDestroy(c->band_st);
-    }
-    for (hipEvent_t e : {c->ev_b0, c->ev_b2})
+    for (hipStream_t st : {c->band_st, c->deep_st})
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+    for (hipEvent_t e : {c->ev_b0, c->ev_b1, c->ev_b2})
         if (e) (void)hipEventDestroy(e);
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
     if (c->ev_int) (void)hipEventDestroy(c->ev_int);
@@ -1124,7 +1185,7 @@ void iblb_destroy(iblb_ctx* c) {
     if (c->g_alloc) (void)hipFree(c->g_alloc);
     void* bufs[] = {c->cil_samples, c->cil_lasts, c->cil_bpoints, c->s_alloc, c->d_band,
                     c->halo_alloc, c->rho0, c->u0, c->force0, c->d_s, c->d_us, c->d_Fs,
-                    c->d_eps, c->d_Fs_sum, c->fdense, c->flags, c->d_Q};
+                    c->d_eps, c->d_Fs_sum, c->fdense, c->flags, c->d_Q, c->d_sch_s, c->d_sch_us, c->d_sch_eps};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1200,11 +1261,13 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
 
 }  // extern "C"
 
-// Streams of the overlapped band cycle (lone slab): the band chain on its own stream restricted
-// to `band_reserve` CUs (whole XCDs at the top, like the RCCL comm stream's), the compute stream
-// (deep sweeps, everything else) masked to the other CUs.  Default: one XCD, two where the band
-// trapezoids hold more than 5 % of the cycle's lattice updates (one-step launches, HBM-bound; the
-// deep sweep is issue-bound).  IBLB_BAND_RESERVE_CUS=0: both on the compute stream, in sequence.
+// Streams of the overlapped band cycle (lone slab): the band chain on band_st restricted to
+// `band_reserve` CUs (whole XCDs at the top, like the RCCL comm stream's), the cycle's deep sweep
+// on deep_st masked to the other CUs.  The context's stream is never replaced: it keeps the
+// whole chip for every other launch and joins the two with events in band_step.  Default: one
+// XCD, two where the band trapezoids hold more than 5 % of the cycle's lattice updates (one-step
+// launches, HBM-bound; the deep sweep is issue-bound).  IBLB_BAND_RESERVE_CUS=0: both on the
+// context's stream, in sequence.
 static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
     if (c->transport != TR_NONE || c->comm_stream) return IBLB_OK;  // RCCL groups keep their streams
     if (!c->ncu) {
@@ -1216,45 +1279,53 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
     const double share = (double)band_cols / (double)std::max(1LL, band_cols + (long long)c->sweep_depth * deep_cols);
     long want = env_long("IBLB_BAND_RESERVE_CUS", (share > 0.05 ? 2 : 1) * per_xcd);
     if (want < 0 || want >= c->ncu) want = 0;
-    if (want == c->band_reserve) return IBLB_OK;
+    if (want == c->band_reserve || (c->band_sticky && c->band_st)) return IBLB_OK;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (c->band_st) {
-        HIP_TRY(c, hipStreamSynchronize(c->band_st));
-        (void)hipStreamDestroy(c->band_st);
-        c->band_st = nullptr;
-    }
-    hipStream_t compute = nullptr;
+    for (hipStream_t* st : {&c->band_st, &c->deep_st})
+        if (*st) {
+            HIP_TRY(c, hipStreamSynchronize(*st));
+            (void)hipStreamDestroy(*st);
+            *st = nullptr;
+        }
     if (want) {
         std::vector<uint32_t> deep((size_t)(c->ncu + 31) / 32, 0u), band(deep.size(), 0u);
         for (int i = 0; i < c->ncu; ++i) {
             std::vector<uint32_t>& m = i >= c->ncu - want ? band : deep;
             m[(size_t)i / 32] |= 1u << (i % 32);
         }
-        HIP_TRY(c, hipExtStreamCreateWithCUMask(&compute, (uint32_t)deep.size(), deep.data()));
+        HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->deep_st, (uint32_t)deep.size(), deep.data()));
         HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->band_st, (uint32_t)band.size(), band.data()));
-        for (hipEvent_t* e : {&c->ev_b0, &c->ev_b2})
+        for (hipEvent_t* e : {&c->ev_b0, &c->ev_b1, &c->ev_b2})
             if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventDisableSystemFence));
-    } else {
-        HIP_TRY(c, hipStreamCreateWithFlags(&compute, hipStreamNonBlocking));
     }
-    (void)hipStreamDestroy(c->stream);
-    c->stream = compute;
     c->band_reserve = (int)want;
     return IBLB_OK;
 }
 
-// IB band plan of the points s (host copy) for band_step; band_valid stays false where the
-// cycle does not apply (see band_ready) or does not pay (bands over half the lattice, bands
-// within 2(K-1) columns of the lattice edge: the reference's flat-index wrap).
+// IB band plan for band_step from the x coordinates of every point the cycles may see (host
+// copy: the static points, or every entry of a schedule plus the points before it); band_valid
+// stays false where the cycle does not apply (see band_ready) or does not pay (bands over half
+// the lattice, bands within 2(K-1) columns of the lattice edge: the reference's flat-index wrap).
 template <typename T>
-static int plan_bands_t(iblb_ctx* c, int ns, const float* s) {
+static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
     const int K = c->sweep_depth, nx = c->nx, R = 2 * (K - 1);
+    // forced columns [x0-1, x0+1] of every point, as a column mask
+    std::vector<char> forced((size_t)nx, 0);
+    for (float xv : xs) {
+        const double x0 = std::nearbyint((double)xv);
+        if (!(x0 - 1 - R >= 0. && x0 + 1 + R <= nx - 1.)) {
+            c->band_valid = false;
+            return IBLB_OK;
+        }
+        for (int x = (int)x0 - 1; x <= (int)x0 + 1; ++x) forced[(size_t)x] = 1;
+    }
     std::vector<std::pair<int, int>> f;
-    f.reserve((size_t)ns);
-    for (int k = 0; k < ns; ++k) {
-        const double x0 = std::nearbyint((double)s[2 * k]);
-        if (!(x0 - 1 - R >= 0. && x0 + 1 + R <= nx - 1.)) return IBLB_OK;
-        f.push_back({(int)x0 - 1, (int)x0 + 1});
+    for (int x = 0; x < nx;) {
+        if (!forced[(size_t)x]) { ++x; continue; }
+        int e = x;
+        while (e + 1 < nx && forced[(size_t)e + 1]) ++e;
+        f.push_back({x, e});
+        x = e + 1;
     }
     std::sort(f.begin(), f.end());
     std::vector<std::pair<int, int>> b;  // merged forced intervals: trapezoids apart, gaps >= R + 8
@@ -1262,6 +1333,8 @@ static int plan_bands_t(iblb_ctx* c, int ns, const float* s) {
         if (!b.empty() && iv.first - b.back().second - 1 < 2 * R + 8) b.back().second = std::max(b.back().second, iv.second);
         else b.push_back(iv);
     }
+    if (c->band_valid && b == c->band_b) return IBLB_OK;  // the installed plan covers these points
+    c->band_valid = false;
     std::vector<int> tab;
     std::vector<int> off((size_t)K), cnt((size_t)K);
     long long cols = 0;
@@ -1309,15 +1382,21 @@ static int plan_bands_t(iblb_ctx* c, int ns, const float* s) {
             ++nsweep;
         }
     }
-    if (tab.size() > c->band_cap) {
+    if (tab.size() > c->band_cap) {  // grow (rare: sized for the whole lattice at K+1 levels)
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
         if (c->d_band) (void)hipFree(c->d_band);
         c->d_band = nullptr;
         c->band_cap = 0;
-        HIP_TRY(c, hipMalloc(&c->d_band, tab.size() * sizeof(int)));
-        c->band_cap = tab.size();
+        const size_t cap = std::max(tab.size(), (size_t)(K + 1) * nx + 4 * (size_t)nsw + 64);
+        HIP_TRY(c, hipMalloc(&c->d_band, cap * sizeof(int)));
+        c->band_cap = cap;
     }
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    HIP_TRY(c, hipMemcpy(c->d_band, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
+    // in stream order: the previous cycle's launches (which read the old tables) come first,
+    // the next cycle's masked streams start after this copy (band_step's ev_b0)
+    std::vector<int>& hb = c->band_host[c->band_host_i];
+    c->band_host_i ^= 1;
+    hb = tab;
+    HIP_TRY(c, hipMemcpyAsync(c->d_band, hb.data(), hb.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     if (!c->s_alloc) {  // the trapezoid's scratch levels: two buffers laid out like g
         const size_t bytes = (size_t)(2 * c->buf_elems + c->buf_gap + 2 * GUARD) * c->esize;
         rc = alloc_zero(c, (void**)&c->s_alloc, bytes);
@@ -1335,14 +1414,40 @@ static int plan_bands_t(iblb_ctx* c, int ns, const float* s) {
     const int fc = c->cfg.flux_column;
     for (auto& iv : b)
         if (fc >= iv.first - (K - 1) && fc <= iv.second + (K - 1)) c->band_flux = fc;
+    c->band_b = b;
     c->band_valid = true;
     return IBLB_OK;
 }
 
-static int plan_bands(iblb_ctx* c, int ns, const float* s) {
-    c->band_valid = false;
-    if (!c->band_on || ns <= 0 || c->sweep_depth < 3 || !c->sweep_on || c->ncol != c->nx || c->cilia_on) return IBLB_OK;
-    return c->prec == IBLB_PREC_F64 ? plan_bands_t<double>(c, ns, s) : plan_bands_t<float>(c, ns, s);
+static int plan_bands(iblb_ctx* c, const std::vector<float>& xs) {
+    if (!c->band_on || xs.empty() || c->sweep_depth < 3 || !c->sweep_on || c->ncol != c->nx || c->cilia_on) {
+        c->band_valid = false;
+        return IBLB_OK;
+    }
+    return c->prec == IBLB_PREC_F64 ? plan_bands_t<double>(c, xs) : plan_bands_t<float>(c, xs);
+}
+
+// The band plan of the cycle starting at iteration c->t under a schedule: the forces of its K
+// levels come from the points of iterations t-1 .. t+K-2 (the force owed at the start was, or
+// will be, evaluated from iteration t-1's points: the points before the schedule if t = t0).
+static int plan_cycle(iblb_ctx* c) {
+    const int K = c->sweep_depth, ns = c->ns;
+    std::vector<float> xs;
+    xs.reserve((size_t)(K + 1) * ns);
+    for (long long it = c->t - 1; it <= c->t + K - 2; ++it) {
+        if (it < c->sch_t0) {
+            xs.insert(xs.end(), c->sch_x_prev.begin(), c->sch_x_prev.end());
+            continue;
+        }
+        const size_t e = (size_t)sched_entry(c, it);
+        xs.insert(xs.end(), c->sch_x.begin() + e * ns, c->sch_x.begin() + (e + 1) * ns);
+    }
+    return plan_bands(c, xs);
+}
+static std::vector<float> x_coords(int ns, const float* s) {
+    std::vector<float> xs((size_t)ns);
+    for (int k = 0; k < ns; ++k) xs[(size_t)k] = s[2 * k];
+    return xs;
 }
 
 extern "C" {
@@ -1380,7 +1485,74 @@ int iblb_set_lagrangian(iblb_ctx* c, int ns, const float* s, const float* u_s, c
         HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
     c->ns = ns;
-    return plan_bands(c, ns, s);
+    c->sch_n = 0;  // a schedule given ahead ends here
+    c->sch_cur = -1;
+    c->band_sticky = false;
+    c->band_valid = false;
+    return plan_bands(c, x_coords(ns, s));
+}
+
+int iblb_set_lagrangian_steps(iblb_ctx* c, int nsteps, int ns, const float* s, const float* u_s, const int* epsilon) {
+    if (!c || ns < 0 || nsteps < 1) return IBLB_ERR_ARG;
+    if (ns > c->max_points) return fail(c, IBLB_ERR_ARG, "ns exceeds max_points of the context");
+    if (ns > 0 && (!s || !u_s)) return IBLB_ERR_ARG;
+    if (c->cilia_on) return fail(c, IBLB_ERR_STATE, "cilia kinematics active: points come from iblb_set_cilia");
+    const size_t np = (size_t)nsteps * ns;
+    if (ns > 0 && c->ncol != c->nx) {
+        if (c->ncol < 3) return fail(c, IBLB_ERR_ARG, "immersed boundary across slabs needs >= 3 columns per slab");
+        for (size_t k = 0; k < np; ++k) {
+            const double x0 = std::nearbyint((double)s[2 * k]);
+            if (!(x0 >= 0. && x0 <= (double)c->nx))
+                return fail(c, IBLB_ERR_ARG, "slab groups need 0 <= nearbyint(s_x) <= XDIM (main.cu:202-205)");
+        }
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (c->ib_state == IB_PENDING) {  // the force owed to the points before the schedule
+        if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: set points between group steps");
+        int rc = ensure_force(c);
+        if (rc) return rc;
+    }
+    // host copies for the per-cycle band plans: every entry's x, and the points before the
+    // schedule (a force evaluated from them is owed to the first iteration)
+    c->sch_x_prev.clear();
+    if (c->ns > 0 && c->ib_state == IB_READY) {
+        std::vector<float> old(2 * (size_t)c->ns);
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, hipMemcpy(old.data(), c->d_s, old.size() * sizeof(float), hipMemcpyDeviceToHost));
+        c->sch_x_prev = x_coords(c->ns, old.data());
+    }
+    if (ns > 0) {
+        if ((size_t)nsteps > c->sch_cap || ns != c->ns) {
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            for (void* p : {(void*)c->d_sch_s, (void*)c->d_sch_us, (void*)c->d_sch_eps})
+                if (p) (void)hipFree(p);
+            c->d_sch_s = c->d_sch_us = nullptr;
+            c->d_sch_eps = nullptr;
+            c->sch_cap = 0;
+            const size_t cap = (size_t)nsteps * c->max_points;
+            HIP_TRY(c, hipMalloc(&c->d_sch_s, 2 * cap * sizeof(float)));
+            HIP_TRY(c, hipMalloc(&c->d_sch_us, 2 * cap * sizeof(float)));
+            HIP_TRY(c, hipMalloc(&c->d_sch_eps, cap * sizeof(int)));
+            c->sch_cap = (size_t)nsteps;
+        }
+        HIP_TRY(c, hipMemcpyAsync(c->d_sch_s, s, 2 * np * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->d_sch_us, u_s, 2 * np * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        if (epsilon) {
+            HIP_TRY(c, hipMemcpyAsync(c->d_sch_eps, epsilon, np * sizeof(int), hipMemcpyHostToDevice, c->stream));
+        } else {
+            std::vector<int> ones(np, 1);
+            HIP_TRY(c, hipMemcpyAsync(c->d_sch_eps, ones.data(), np * sizeof(int), hipMemcpyHostToDevice, c->stream));
+        }
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        c->sch_x = x_coords((int)np, s);
+    }
+    c->ns = ns;
+    c->sch_t0 = c->t;
+    c->sch_n = ns > 0 ? nsteps : 0;
+    c->sch_cur = -1;  // d_s still holds the points before the schedule (their force is READY)
+    c->band_sticky = true;
+    c->band_valid = false;  // planned per cycle (plan_cycle)
+    return IBLB_OK;
 }
 
 static int reset_cilia_state(iblb_ctx* c) {
@@ -1395,6 +1567,8 @@ static int reset_cilia_state(iblb_ctx* c) {
 int iblb_set_cilia(iblb_ctx* c, const iblb_cilia* k) {
     if (!c) return IBLB_ERR_ARG;
     c->band_valid = false;  // the points now come from the kinematics
+    c->sch_n = 0;
+    c->sch_cur = -1;
     HIP_TRY(c, hipSetDevice(c->device));
     if (c->ib_state == IB_PENDING) {  // force still owed to the current points
         if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: set cilia between group steps");
@@ -1441,6 +1615,9 @@ int iblb_step(iblb_ctx* c, int nsteps) {
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
     for (int s = 0; s < nsteps;) {
+        if (c->sch_n > 0 && !c->cilia_on && c->phase == PH_RUN && nsteps - s >= c->sweep_depth &&
+            (rc = plan_cycle(c)))
+            return rc;
         if (nsteps - s >= c->sweep_depth && band_ready(c)) {
             if ((rc = c->prec == IBLB_PREC_F64 ? band_step<double>(c) : band_step<float>(c))) return rc;
             s += c->sweep_depth;
@@ -2043,7 +2220,7 @@ int iblb_load_checkpoint(iblb_ctx* c, const char* path) {
     if (ns > 0 && !c->cilia_on) {  // the band plan of the restored points
         std::vector<float> hs(2 * ns);
         HIP_TRY(c, hipMemcpy(hs.data(), c->d_s, hs.size() * sizeof(float), hipMemcpyDeviceToHost));
-        if ((rc = plan_bands(c, (int)ns, hs.data()))) return rc;
+        if ((rc = plan_bands(c, x_coords((int)ns, hs.data())))) return rc;
     }
     c->t = iv[CK_T];
     c->phase = PH_RUN;

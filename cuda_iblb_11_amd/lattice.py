@@ -178,6 +178,22 @@ class Lattice:
         self._check(self._lib.iblb_set_lagrangian(self._h, ns, _ptr(s), _ptr(u_s), _ptr(eps)))
         self.ns = ns
 
+    def set_lagrangian_steps(self, s, u_s, epsilon=None) -> None:
+        """Points of the next n iterations given ahead (iblb_set_lagrangian_steps): s, u_s of
+        shape (n, 2*Ns) (float32 xy), epsilon (n, Ns) or None; iteration steps+i uses row i."""
+        s = np.ascontiguousarray(s, dtype=np.float32)
+        u_s = np.ascontiguousarray(u_s, dtype=np.float32)
+        if s.ndim != 2 or s.shape != u_s.shape or s.shape[1] % 2:
+            raise ValueError("s and u_s must both have shape (nsteps, 2*Ns)")
+        n, ns = s.shape[0], s.shape[1] // 2
+        eps = None
+        if epsilon is not None:
+            eps = np.ascontiguousarray(epsilon, dtype=np.int32)
+            if eps.shape != (n, ns):
+                raise ValueError("epsilon must have shape (nsteps, Ns)")
+        self._check(self._lib.iblb_set_lagrangian_steps(self._h, n, ns, _ptr(s), _ptr(u_s), _ptr(eps)))
+        self.ns = ns
+
     def set_cilia(self, c_num: int, c_space: float, T: int, p_step: int) -> None:
         """Run the reference's cilia kinematics on the device every iteration (main.cu:822-841);
         c_num = 0 switches it off.  Needs max_points >= 96 * c_num."""

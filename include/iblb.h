@@ -171,6 +171,16 @@ int iblb_set_state(iblb_ctx* ctx, const double* rho, const double* u, const doub
 int iblb_set_lagrangian(iblb_ctx* ctx, int ns, const float* s, const float* u_s,
                         const int* epsilon);
 
+/* Lagrangian points of the next `nsteps` iterations, given ahead (the reference computes a
+ * new s, u_s, epsilon every iteration before its IB step, main.cu:822-841, 900-909): iteration
+ * t0 + i (t0 = iblb_get_step at the call) uses entry i; after the last entry the points stay
+ * those of entry nsteps-1.  Same result as iblb_set_lagrangian(entry i) before each of those
+ * iterations, but iblb_step can then advance several iterations per launch (IB band cycle)
+ * where the points of one cycle force only part of the lattice.  s, u_s [nsteps][2ns] xy,
+ * epsilon [nsteps][ns] (NULL = all 1).  iblb_set_lagrangian / iblb_set_cilia end the schedule. */
+int iblb_set_lagrangian_steps(iblb_ctx* ctx, int nsteps, int ns, const float* s, const float* u_s,
+                              const int* epsilon);
+
 /* On-device cilia kinematics (main.cu:822-841): when set, every iblb_step iteration `it`
  * first runs define_filament + boundary_check for `it` and uses their s, u_s, epsilon as the
  * Lagrangian points of that iteration (no host round trip).  c_num <= 0 or NULL disables.

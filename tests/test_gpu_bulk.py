@@ -1,0 +1,262 @@
+"""Bulk stepping at the BASELINE.json sizes against the oracle (oracle_step = main.cu:852-909,
+one reference iteration at a time), on PERTURBED states: every lat.step(n) here advances many
+iterations in one call, so the K-iteration deep sweeps (lbm_sweep.hip), their remainders (two-
+iteration sweeps, one-step launches) and the IB band cycle run exactly as in production, and
+their result is compared with the restatement directly (not only with one-step launches).
+
+Configs (BASELINE.json): K1 128^2 f64 1000 steps; K2 2048^2 f64; K4 8192x2048
+f64; M 4096^2 f64; K5 8192x2048 f32 + 64 filaments x 96 points moving every iteration (points
+given ahead with iblb_set_lagrangian_steps, band cycle), the oracle with its point-centric spread
+(bit-identical to the reference's cell-centric gather, tests/test_oracle.py).
+
+Tolerances (north star): max|phi - phi_ref| / max|phi_ref| <= 1e-6 (f64), 1e-4 (f32) for
+phi in {rho, u_x, u_y}; the f64 tests also hold a much tighter engineering bound.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL64, TOL32, TIGHT = 1e-6, 1e-4, 1e-9
+
+
+def rel(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    m = np.max(np.abs(b))
+    return float(np.max(np.abs(a - b)) / (m if m > 0 else 1.0))
+
+
+def fields(lat, sim):
+    rho, u = lat.macro()
+    N = lat.N
+    return {"rho": rel(rho, sim.rho), "rho-1": rel(rho - 1, sim.rho - 1), "ux": rel(u[:N], sim.u[:N]),
+            "uy": rel(u[N:], sim.u[N:])}
+
+
+@pytest.fixture(scope="module")
+def threads(oracle):
+    oracle.set_threads(min(16, os.cpu_count() or 1))
+    yield
+    oracle.set_threads(1)
+
+
+def bulk_pair(P, O, nx, ny, chunks, *, precision="f64", seed=31):
+    """Channel (body force, no IB) from a perturbed state; the GPU steps in the given chunks, the
+    oracle one iteration at a time.  Returns (lat, sim, timing)."""
+    from cuda_iblb_11_amd import workloads as W
+    rho, u = W.perturbed_state(nx, ny, seed)
+    sim = O.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=W.BODY_FORCE)
+    lat = P.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=W.BODY_FORCE)
+    lat.set_state(rho, u)
+    del rho, u
+    lat.set_profiling(True)
+    for n in chunks:
+        lat.step(n)
+    sim.step(sum(chunks))
+    return lat, sim, lat.timing()
+
+
+def test_k1_1000_steps_bulk(gpu, oracle, threads):
+    """K1: 128 x 128, 1000 iterations in one call (boot + 199 deep launches + remainder): the
+    longest horizon of the deep sweep against the restatement."""
+    lat, sim, tm = bulk_pair(gpu, oracle, 128, 128, [1000])
+    assert tm["sweepk_launches"] >= 190, tm
+    r = fields(lat, sim)
+    assert max(r["rho"], r["ux"], r["uy"]) <= TIGHT, r
+    assert r["rho-1"] <= 1e-8, r
+    assert abs(lat.flux - sim.flux) <= TIGHT * abs(sim.flux)
+
+
+def test_k2_bulk(gpu, oracle, threads):
+    """K2: 2048^2 f64, 23 iterations in chunks that mix deep launches and remainders."""
+    lat, sim, tm = bulk_pair(gpu, oracle, 2048, 2048, [1, 10, 7, 5])
+    assert tm["sweepk_launches"] >= 3, tm
+    r = fields(lat, sim)
+    assert max(r["rho"], r["ux"], r["uy"]) <= TIGHT, r
+    assert abs(lat.flux - sim.flux) <= TIGHT * abs(sim.flux)
+
+
+def test_k4_bulk(gpu, oracle, threads):
+    """K4: 8192 x 2048 f64 (one GPU), 11 iterations: boot + two deep launches."""
+    lat, sim, tm = bulk_pair(gpu, oracle, 8192, 2048, [11])
+    assert tm["sweepk_launches"] == 2, tm
+    r = fields(lat, sim)
+    assert max(r["rho"], r["ux"], r["uy"]) <= TIGHT, r
+    assert abs(lat.flux - sim.flux) <= TIGHT * abs(sim.flux)
+
+
+def test_m_bulk_perturbed(gpu, oracle, threads):
+    """M: 4096^2 f64 (the metric config) from a perturbed, not x-uniform, state, 11 iterations."""
+    lat, sim, tm = bulk_pair(gpu, oracle, 4096, 4096, [11])
+    assert tm["sweepk_launches"] == 2, tm
+    r = fields(lat, sim)
+    assert max(r["rho"], r["ux"], r["uy"]) <= TIGHT, r
+
+
+def test_m_bulk_f32(gpu, oracle, threads):
+    lat, sim, tm = bulk_pair(gpu, oracle, 4096, 4096, [11], precision="f32")
+    assert tm["sweepk_launches"] == 2, tm
+    r = fields(lat, sim)
+    assert max(r["rho"], r["ux"], r["uy"]) <= TOL32, r
+
+
+def _schedule(points, t0, n):
+    """Stack points(it) for it = t0 .. t0+n-1 into (n, 2Ns) / (n, Ns) arrays."""
+    ent = [points(it) for it in range(t0, t0 + n)]
+    return (np.stack([e[0] for e in ent]), np.stack([e[1] for e in ent]), np.stack([e[2] for e in ent]))
+
+
+def moving_run(P, O, nx, ny, points, chunks, *, precision="f64", body_force=(0.0, 0.0), seed=13, band=1,
+               monkeypatch=None, readers=False):
+    """Points that move every iteration, given ahead per chunk (iblb_set_lagrangian_steps) on the
+    GPU and set per iteration on the oracle (main.cu:822-909 order)."""
+    from cuda_iblb_11_amd import workloads as W
+    if monkeypatch is not None:
+        monkeypatch.setenv("IBLB_IB_BAND", str(band))
+    rho, u = W.perturbed_state(nx, ny, seed)
+    ns = points(0)[0].size // 2
+    sim = O.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=body_force)
+    lat = P.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=body_force, max_points=ns)
+    lat.set_state(rho, u)
+    lat.set_profiling(True)
+    t = 0
+    for n in chunks:
+        lat.set_lagrangian_steps(*_schedule(points, t, n))
+        lat.step(n)
+        for it in range(t, t + n):
+            sim.set_lagrangian(*points(it))
+            sim.step(1)
+        t += n
+        if readers:
+            lat.macro()
+            lat.force()
+    return lat, sim
+
+
+def _swaying(nx, n_fil=2, pts=48, period=30):
+    """Filaments whose points move every iteration (x sways by up to +-2 columns)."""
+    def points(it):
+        k = np.arange(pts)
+        s_all, u_all, e_all = [], [], []
+        for m in range(n_fil):
+            ph = 2 * np.pi * (it + 7 * m) / period
+            s = np.empty(2 * pts, np.float32)
+            s[0::2] = (m + 0.5) * nx / n_fil + 0.37 + 2.0 * (k / pts) * np.sin(ph)
+            s[1::2] = 2.0 + k
+            us = np.zeros(2 * pts, np.float32)
+            us[0::2] = 2.0 * (k / pts) * np.cos(ph) * 2 * np.pi / period * 0.05
+            us[1::2] = 1e-4 * np.sin(ph)
+            s_all.append(s)
+            u_all.append(us)
+            e_all.append((k % 11 != 5).astype(np.int32))
+        return np.concatenate(s_all), np.concatenate(u_all), np.concatenate(e_all)
+    return points
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_moving_points_band_cycle_matches_oracle(gpu, oracle, precision, monkeypatch):
+    """Points that move every iteration through the IB band cycle: the schedule's forced columns
+    make the bands, each level's IB uses its own iteration's points; readers between chunks."""
+    nx, ny = 320, 128
+    lat, sim = moving_run(gpu, oracle, nx, ny, _swaying(nx), [1, 12, 5, 3, 15], precision=precision,
+                          monkeypatch=monkeypatch, readers=True)
+    tm = lat.timing()
+    assert tm["sweepk_launches"] >= 6, tm  # band cycles ran (one deep sweep each)
+    r = fields(lat, sim)
+    tol = 1e-10 if precision == "f64" else TOL32
+    assert max(r["rho"], r["ux"], r["uy"]) <= tol, r
+    assert rel(lat.force(), sim.force) <= (1e-9 if precision == "f64" else 1e-3)
+    assert rel(lat.lagrangian_force(), sim.F_s) <= (1e-5 if precision == "f64" else 1e-2)
+    assert abs(lat.flux - sim.flux) <= (1e-9 if precision == "f64" else 1e-4) * max(abs(sim.flux), 1e-30)
+    s, us, eps = lat.lagrangian()  # the current points are the last iteration's
+    s_ref, us_ref, eps_ref = _swaying(nx)(lat.steps - 1)
+    assert np.array_equal(s, s_ref) and np.array_equal(us, us_ref) and np.array_equal(eps, eps_ref)
+
+
+def test_schedule_equals_per_iteration_points(gpu, oracle, monkeypatch):
+    """A schedule given ahead equals iblb_set_lagrangian before every iteration: with the band
+    cycle off (same launches) and on (K-iteration cycles), up to the spread atomics' order."""
+    nx, ny = 256, 96
+    pts = _swaying(nx, n_fil=3, pts=40)
+    from cuda_iblb_11_amd import workloads as W
+    rho, u = W.perturbed_state(nx, ny, 5)
+    ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, max_points=120)
+    ref.set_state(rho, u)
+    for it in range(27):
+        ref.set_lagrangian(*pts(it))
+        ref.step(1)
+    r0, u0 = ref.macro()
+    for band in ("0", "1"):
+        monkeypatch.setenv("IBLB_IB_BAND", band)
+        lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, max_points=120)
+        lat.set_state(rho, u)
+        lat.set_profiling(True)
+        lat.set_lagrangian_steps(*_schedule(pts, 0, 27))
+        lat.step(27)
+        r1, u1 = lat.macro()
+        assert rel(r1, r0) <= 1e-13 and rel(u1, u0) <= 1e-12, band
+        assert (lat.timing()["sweepk_launches"] > 0) == (band == "1")
+        lat.close()
+
+
+def test_k3_time_varying_filament(gpu, oracle, threads):
+    """K3 as SURVEY.md §8(d) prescribes it: 2048^2 f64, one 256-point filament at x = 1024 with
+    u_s(it) = (U0 (k/255) sin(2 pi it / T), 0) changing every iteration; 12 iterations in one
+    call through the band cycle."""
+    from cuda_iblb_11_amd import workloads as W
+    pts = lambda it: W.filament(it, n_points=256, x0=1024.0, y0=1.0, dy=1.0, U0=1e-3, period=20)
+    lat, sim = moving_run(gpu, oracle, 2048, 2048, pts, [12])
+    assert lat.timing()["sweepk_launches"] >= 2
+    r = fields(lat, sim)
+    assert max(r["rho"], r["ux"], r["uy"]) <= 1e-10, r
+    assert abs(lat.flux - sim.flux) <= 1e-9 * max(abs(sim.flux), 1e-30)
+
+
+def test_k5_filament_array_f32(gpu, oracle, threads):
+    """K5 on one GPU: 8192 x 2048 f32 + 64 filaments x 96 points (6144) that move every
+    iteration (W.filament_array(it)), 11 iterations in one call: boot + two band cycles."""
+    from cuda_iblb_11_amd import workloads as W
+    pts = lambda it: W.filament_array(it, 8192, n_fil=64, pts=96, period=200)
+    lat, sim = moving_run(gpu, oracle, 8192, 2048, pts, [11], precision="f32", body_force=W.BODY_FORCE)
+    assert lat.timing()["sweepk_launches"] == 2
+    r = fields(lat, sim)
+    assert max(r["rho"], r["ux"], r["uy"]) <= TOL32, r
+
+
+def test_band_streams_keep_the_context_stream(gpu, monkeypatch):
+    """A band plan (masked streams for the band chain and the deep sweep) must not replace the
+    context's stream: iblb_get_stream keeps its handle, and once the points are gone the no-IB
+    deep sweeps run on the full chip, bit-identical to a context that never had points."""
+    from cuda_iblb_11_amd import workloads as W
+    nx, ny = 256, 96
+    rho, u = W.perturbed_state(nx, ny, 2)
+    k = np.arange(30)
+    s = np.empty(60, np.float32)
+    s[0::2], s[1::2] = 100.3, 3.0 + k
+    us = np.full(60, 1e-4, np.float32)
+    ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, body_force=W.BODY_FORCE, max_points=30)
+    lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, body_force=W.BODY_FORCE, max_points=30)
+    for x in (ref, lat):
+        x.set_state(rho, u)
+    stream0 = lat.stream
+    lat.set_lagrangian(s, us)
+    lat.set_profiling(True)
+    lat.step(11)  # boot + two band cycles
+    assert lat.timing(reset=True)["sweepk_launches"] == 2  # the band cycle ran on its streams
+    assert lat.stream == stream0
+    lat.set_lagrangian(np.zeros(0, np.float32), np.zeros(0, np.float32))  # points gone
+    ref.set_lagrangian(s, us)
+    monkeypatch.setenv("IBLB_IB_BAND", "0")
+    ref2 = gpu.Lattice(nx, ny, W.TAU, W.TAU2, body_force=W.BODY_FORCE, max_points=30)
+    ref2.set_state(rho, u)
+    ref2.set_lagrangian(s, us)
+    ref2.step(11)
+    ref2.set_lagrangian(np.zeros(0, np.float32), np.zeros(0, np.float32))
+    lat.step(25)
+    ref2.step(25)
+    assert lat.timing()["sweepk_launches"] == 5
+    r1, u1 = lat.macro()
+    r2, u2 = ref2.macro()
+    assert rel(r1, r2) <= 1e-13 and rel(u1, u2) <= 1e-12

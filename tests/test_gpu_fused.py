@@ -563,7 +563,9 @@ def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch)
     for name in ("IBLB_SWEEP_VS", "IBLB_SWEEP_W", "IBLB_SWEEP_VARIANT", "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT",
                  "IBLB_SWEEP_DEPTH"):
         monkeypatch.delenv(name)
-    lat, sim = run_pair(gpu, oracle, 70, 125, 40, precision=precision)  # default (deep) sweeps vs the oracle
+    # (run_pair steps one iteration per call: one-step launches vs the oracle; the sweeps against
+    # the oracle in bulk: tests/test_gpu_bulk.py)
+    lat, sim = run_pair(gpu, oracle, 70, 125, 40, precision=precision)
     check_fields(lat, sim, TIGHT if precision == "f64" else TOL32)
 
 
@@ -642,11 +644,11 @@ def test_ib_band_equals_one_step_path(gpu, oracle, monkeypatch):
         lat, sim = _static_run(gpu, oracle, nx, ny, 30, pts, chunks=(3, 5, 7, 5, 10), band=band,
                                monkeypatch=monkeypatch)
         runs[band] = (lat.macro(), lat.force(), lat.flux, lat.timing()["sweepk_launches"])
+        check_fields(lat, sim, 1e-10)  # each run against the oracle, the band run included
     assert runs[1][3] >= 4 and runs[0][3] == 0
     (r1, u1), (r0, u0) = runs[1][0], runs[0][0]
     assert rel(r1, r0) <= 1e-13 and rel(u1, u0) <= 1e-12
     assert rel(runs[1][1], runs[0][1]) <= 1e-12
-    check_fields(lat, sim, 1e-10)
 
 
 def test_ib_band_declined_near_edges(gpu, oracle, monkeypatch):
