@@ -48,13 +48,41 @@ WORKLOADS = {
 
 
 def workload_points(kind, nx):
-    """Static Lagrangian points (positions and velocities fixed, IB evaluated every step)."""
+    """Lagrangian points of iteration `it` (a function), IB evaluated every iteration:
+    K3: one 256-point filament at x = nx/2, u_s = (U0 (k/255) sin(2 pi it/T), 0)
+    changing every iteration; K5: 64 filaments x 96 points (W.filament_array) whose points move
+    every iteration (tilt up to 8 columns over the period T = 1000)."""
     from cuda_iblb_11_amd import workloads as W
     if kind == "filament":
-        return W.filament(250, n_points=256, x0=nx / 2 + 0.3, y0=1.0, dy=1.0, U0=1e-3, period=1000)
+        return lambda it: W.filament(it, n_points=256, x0=nx / 2 + 0.3, y0=1.0, dy=1.0, U0=1e-3, period=1000)
     if kind == "array":
-        return W.filament_array(250, nx, n_fil=64, pts=96)
+        return lambda it: W.filament_array(it, nx, n_fil=64, pts=96, period=1000)
     return None
+
+
+class Driver:
+    """lat.step(n) with the workload's points of those n iterations given ahead
+    (iblb_set_lagrangian_steps: staged in HBM before the launches, like the reference's
+    per-iteration cilia positions that its kinematics kernels write to the device); --frozen:
+    the points of iteration 250 for the whole run (round-1 workload)."""
+
+    def __init__(self, lat, points, frozen):
+        self.lat, self.points, self.frozen, self.t = lat, points, frozen, 0
+        if points is not None and frozen:
+            lat.set_lagrangian(*points(250))
+
+    def stage(self, n):
+        if self.points is None or self.frozen:
+            return
+        ent = [self.points(it) for it in range(self.t, self.t + n)]
+        self.lat.set_lagrangian_steps(np.stack([e[0] for e in ent]), np.stack([e[1] for e in ent]),
+                                      np.stack([e[2] for e in ent]))
+
+    def run(self, n, staged=False):
+        if not staged:
+            self.stage(n)
+        self.lat.step(n)
+        self.t += n
 
 
 def parse():
@@ -73,6 +101,8 @@ def parse():
     p.add_argument("--prime-seconds", type=float, default=1.0,
                    help="untimed steps before the warmup until this much wall time has passed (the GPU "
                         "clock settles under load; reported as `prime` in the JSON line)")
+    p.add_argument("--frozen", action="store_true",
+                   help="IB workloads: points of iteration 250 for the whole run (round-1 workload)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU sample duration")
     p.add_argument("--no-profile-events", action="store_true", help="skip per-launch HIP events")
@@ -83,7 +113,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(nx, ny, budget_s, points=None):
+def cpu_baseline(nx, ny, budget_s, points=None, frozen=False):
     """The reference's own unfused sequence (equilibrium, collision, streaming, macro,
     interpolate + the literal O(N*Ns) spread gather when there are points; AoS fp64) restated in
     C (oracle/), OpenMP over the host cores, timed on a bounded number of steps of the same
@@ -105,22 +135,31 @@ def cpu_baseline(nx, ny, budget_s, points=None):
         O.load()
         native = False
     O.set_threads(threads)
-    ns = 0 if points is None else points[0].size // 2
+    ns = 0 if points is None else points(0)[0].size // 2
     est = nx * ny * ns * 2e-8 / threads  # ~20 ns per delta evaluation and core
     if est > 90:
         return {"value": None, "unit": "MLUPS", "cores": threads, "kind": kind, "node": node,
                 "sample": f"skipped: the reference's O(N*Ns) spread needs ~{est:.0f} s per step on {threads} cores"}
     rho, u = W.perturbed_state(nx, ny, W.SEED)
     sim = O.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=W.BODY_FORCE, point_spread=False)
-    if points is not None:
-        sim.set_lagrangian(*points)
     del rho, u
+
+    def steps(t, n):  # the points of every iteration set before it (set once if frozen)
+        if points is None or frozen:
+            if points is not None and t == 0:
+                sim.set_lagrangian(*points(250))
+            sim.step(n)
+            return
+        for it in range(t, t + n):
+            sim.set_lagrangian(*points(it))
+            sim.step(1)
+
     t0 = time.perf_counter()
-    sim.step(1)  # warm-up + size the sample
+    steps(0, 1)  # warm-up + size the sample
     one = time.perf_counter() - t0
     n = int(max(1, min(50, budget_s / max(one, 1e-6))))
     t0 = time.perf_counter()
-    sim.step(n)
+    steps(1, n)
     dt = time.perf_counter() - t0
     mlups = nx * ny * n / dt / 1e6
     return {"value": round(mlups, 3), "unit": "MLUPS", "cores": threads, "kind": kind, "node": node,
@@ -215,7 +254,7 @@ def main():
         nx *= world
     precision = a.precision or wprec
     points = workload_points(wpts, nx)
-    ns = 0 if points is None else points[0].size // 2
+    ns = 0 if points is None else points(0)[0].size // 2
     xb, xc = P.plan_slabs(nx, world)[rank]
     lat = P.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=W.BODY_FORCE, device=local,
                     x_begin=xb, x_count=xc if world > 1 else 0, max_points=ns)
@@ -229,8 +268,7 @@ def main():
     elif a.rccl_self:
         os.environ["IBLB_RCCL_SELF"] = "1"
         lat.attach_rccl(P.rccl_unique_id(), 1, 0)
-    if points is not None:
-        lat.set_lagrangian(*points)
+    drv = Driver(lat, points, a.frozen)
 
     # prime: the clock of an idle GPU ramps up over the first ~0.1-1 s of load; a 20-step timed
     # region (~3 ms at 4096^2) would otherwise measure the ramp (profiles/r02a_bench_*.json: 109k
@@ -245,11 +283,14 @@ def main():
             go = bool(flag.item() > 0)
         if not go:
             break
-        lat.step(50)
+        drv.run(50)
         lat.synchronize()
         prime_steps += 50
     prime_s = time.perf_counter() - tp
-    lat.step(a.warmup)
+    # the points of the warmup and the timed steps given ahead in one schedule: nothing of the
+    # timed iterations (not even the force owed at its start) is evaluated before the timer
+    drv.stage(a.warmup + a.steps)
+    drv.run(a.warmup, staged=True)
     lat.synchronize()
     # Launch timing for the roofline: HIP events around every collide launch.  At N = 1 without
     # IB they bracket the launches of the timed region itself (one sweep launch per two steps:
@@ -267,14 +308,14 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    lat.step(a.steps)
+    drv.run(a.steps, staged=True)
     lat.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     tm = lat.timing(reset=True)
     if not events_in_timed and not a.no_profile_events:
         lat.set_profiling(True)
-        lat.step(min(a.steps, 100))
+        drv.run(min(a.steps, 100))
         lat.synchronize()
         tm = lat.timing(reset=True)
         lat.set_profiling(False)
@@ -332,7 +373,7 @@ def main():
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
             lat.close()
-            cpu = cpu_baseline(nx, ny, a.cpu_seconds, points)
+            cpu = cpu_baseline(nx, ny, a.cpu_seconds, points, a.frozen)
         out = {
             "metric": METRIC,
             "value": round(mlups, 2),
@@ -352,7 +393,11 @@ def main():
                             + (f"{iters_per_launch} iterations per launch (pull-stream+collide {iters_per_launch} times, "
                                "intermediate states in registers)" if sweep else
                                "one fused pull-stream+collide launch per step")
-                            + (f"; IB: {ns} static Lagrangian points, interpolate+spread every step" if ns else "")
+                            + ((f"; IB: {ns} Lagrangian points, interpolate+spread every step, " +
+                                ("points frozen at iteration 250 (--frozen)" if a.frozen else
+                                 "points of every iteration given ahead (iblb_set_lagrangian_steps): "
+                                 + ("fixed positions, u_s(it)" if wpts == "filament" else "moving positions")))
+                               if ns else "")
                             + ("; IB band cycle: columns within K-1 of a forced column one iteration per launch, "
                                "the rest in the deep sweep" if ns and tm["sweepk_launches"] else ""),
                 "nx": nx, "ny": ny, "global_cells": cells, "ib_points": ns,

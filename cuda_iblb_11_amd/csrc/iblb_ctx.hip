@@ -110,8 +110,11 @@ struct iblb_ctx {
     std::vector<float> sch_x;       // [sch_n][ns]
     std::vector<float> sch_x_prev;  // the points before the schedule (their force may be owed)
     std::vector<std::pair<int, int>> band_b;  // merged forced intervals of the installed plan
-    std::vector<int> band_host[2];            // host staging of the uploaded tables (alternating)
-    int band_host_i = 0;
+    // pinned host staging of the uploaded tables: a ring, each slot reused only after its copy
+    int* band_pin[4] = {nullptr, nullptr, nullptr, nullptr};
+    size_t band_pin_cap = 0;  // ints per slot
+    hipEvent_t band_pin_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int band_pin_i = 0;
     bool band_sticky = false;                 // keep the reserved XCDs while a schedule runs
     double* fdense = nullptr;
     uint8_t* flags = nullptr;
@@ -216,18 +219,19 @@ int sched_entry(const iblb_ctx* c, long long it) {
 template <typename P>
 P* sched_ptr(P* base, const iblb_ctx* c, int e, int per_point) { return base + (size_t)e * per_point * c->ns; }
 
-// the current points become those of schedule entry e (copies on the context's stream)
+// the current points become those of schedule entry e (no copy: the IB launches and readers
+// take the entry's arrays, pts_*)
 int sched_use(iblb_ctx* c, int e) {
-    if (c->sch_n <= 0 || e == c->sch_cur) return IBLB_OK;
-    const size_t ns = (size_t)c->ns;
-    HIP_TRY(c, hipMemcpyAsync(c->d_s, sched_ptr(c->d_sch_s, c, e, 2), 2 * ns * sizeof(float), hipMemcpyDeviceToDevice,
-                              c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->d_us, sched_ptr(c->d_sch_us, c, e, 2), 2 * ns * sizeof(float),
-                              hipMemcpyDeviceToDevice, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->d_eps, sched_ptr(c->d_sch_eps, c, e, 1), ns * sizeof(int), hipMemcpyDeviceToDevice,
-                              c->stream));
-    c->sch_cur = e;
+    if (c->sch_n > 0) c->sch_cur = e;
     return IBLB_OK;
+}
+// arrays of the current points: the schedule entry in use, else the static points
+const float* pts_s(const iblb_ctx* c) { return c->sch_n > 0 && c->sch_cur >= 0 ? sched_ptr(c->d_sch_s, c, c->sch_cur, 2) : c->d_s; }
+const float* pts_us(const iblb_ctx* c) {
+    return c->sch_n > 0 && c->sch_cur >= 0 ? sched_ptr(c->d_sch_us, c, c->sch_cur, 2) : c->d_us;
+}
+const int* pts_eps(const iblb_ctx* c) {
+    return c->sch_n > 0 && c->sch_cur >= 0 ? sched_ptr(c->d_sch_eps, c, c->sch_cur, 1) : c->d_eps;
 }
 
 // periodic images of a lone slab: the edge columns of the buffer g itself
@@ -393,8 +397,8 @@ int pack_send(iblb_ctx* c) {
 // here: the collide that consumed the previous force cleared both.
 template <typename T>
 int ib_single(iblb_ctx* c) {
-    HIP_TRY(c, launch_ib_point<T>(gptr<T>(c, c->cur), c->L, halo_of<T>(c, c->cur), c->nx, c->ns, c->d_s, c->d_us,
-                                  c->d_eps, c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream));
+    HIP_TRY(c, launch_ib_point<T>(gptr<T>(c, c->cur), c->L, halo_of<T>(c, c->cur), c->nx, c->ns, pts_s(c), pts_us(c),
+                                  pts_eps(c), c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream));
     c->ib_state = IB_READY;
     return IBLB_OK;
 }
@@ -403,7 +407,7 @@ int ib_single(iblb_ctx* c) {
 template <typename T>
 int ib_slab(iblb_ctx* c) {
     IbHalo<T> X{(const T*)c->recv_left, (const T*)c->recv_right};
-    HIP_TRY(c, launch_ib_slab<T>(gptr<T>(c, c->cur), c->L, X, c->nx, c->x_begin, c->ns, c->d_s, c->d_us, c->d_eps,
+    HIP_TRY(c, launch_ib_slab<T>(gptr<T>(c, c->cur), c->L, X, c->nx, c->x_begin, c->ns, pts_s(c), pts_us(c), pts_eps(c),
                                  c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream));
     c->ib_state = IB_READY;
     return IBLB_OK;
@@ -721,7 +725,7 @@ int band_step(iblb_ctx* c) {
     if (c->ib_state == IB_PENDING) {  // force^t from g^t
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, bs))) return rc;
-        HIP_TRY(c, launch_ib_point<T>(A, c->L, halo_at<T>(c, A), c->nx, c->ns, c->d_s, c->d_us, c->d_eps, c->d_Fs,
+        HIP_TRY(c, launch_ib_point<T>(A, c->L, halo_at<T>(c, A), c->nx, c->ns, pts_s(c), pts_us(c), pts_eps(c), c->d_Fs,
                                       c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, bs));
         if ((rc = ev_end(c, ev, EV_IB, 0, bs))) return rc;
         c->ib_state = IB_READY;
@@ -1178,6 +1182,10 @@ void iblb_destroy(iblb_ctx* c) {
         }
     for (hipEvent_t e : {c->ev_b0, c->ev_b1, c->ev_b2})
         if (e) (void)hipEventDestroy(e);
+    for (int i = 0; i < 4; ++i) {
+        if (c->band_pin_ev[i]) (void)hipEventDestroy(c->band_pin_ev[i]);
+        if (c->band_pin[i]) (void)hipHostFree(c->band_pin[i]);
+    }
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
     if (c->ev_int) (void)hipEventDestroy(c->ev_int);
     if (c->ev_pre) (void)hipEventDestroy(c->ev_pre);
@@ -1392,11 +1400,28 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
         c->band_cap = cap;
     }
     // in stream order: the previous cycle's launches (which read the old tables) come first,
-    // the next cycle's masked streams start after this copy (band_step's ev_b0)
-    std::vector<int>& hb = c->band_host[c->band_host_i];
-    c->band_host_i ^= 1;
-    hb = tab;
-    HIP_TRY(c, hipMemcpyAsync(c->d_band, hb.data(), hb.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    // the next cycle's masked streams start after this copy (band_step's ev_b0).  From pinned
+    // memory the copy does not make the host wait for the stream (per-cycle plans of moving
+    // points would otherwise serialise host and device every cycle).
+    if (tab.size() > c->band_pin_cap) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        const size_t cap = std::max(tab.size(), c->band_cap);
+        for (int i = 0; i < 4; ++i) {
+            if (c->band_pin[i]) (void)hipHostFree(c->band_pin[i]);
+            c->band_pin[i] = nullptr;
+        }
+        c->band_pin_cap = 0;
+        for (int i = 0; i < 4; ++i) HIP_TRY(c, hipHostMalloc((void**)&c->band_pin[i], cap * sizeof(int)));
+        c->band_pin_cap = cap;
+    }
+    const int slot = c->band_pin_i;
+    c->band_pin_i = (slot + 1) % 4;
+    if (c->band_pin_ev[slot]) HIP_TRY(c, hipEventSynchronize(c->band_pin_ev[slot]));
+    else HIP_TRY(c, hipEventCreateWithFlags(&c->band_pin_ev[slot], hipEventDisableTiming));
+    std::memcpy(c->band_pin[slot], tab.data(), tab.size() * sizeof(int));
+    HIP_TRY(c, hipMemcpyAsync(c->d_band, c->band_pin[slot], tab.size() * sizeof(int), hipMemcpyHostToDevice,
+                              c->stream));
+    HIP_TRY(c, hipEventRecord(c->band_pin_ev[slot], c->stream));
     if (!c->s_alloc) {  // the trapezoid's scratch levels: two buffers laid out like g
         const size_t bytes = (size_t)(2 * c->buf_elems + c->buf_gap + 2 * GUARD) * c->esize;
         rc = alloc_zero(c, (void**)&c->s_alloc, bytes);
@@ -1518,7 +1543,7 @@ int iblb_set_lagrangian_steps(iblb_ctx* c, int nsteps, int ns, const float* s, c
     if (c->ns > 0 && c->ib_state == IB_READY) {
         std::vector<float> old(2 * (size_t)c->ns);
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        HIP_TRY(c, hipMemcpy(old.data(), c->d_s, old.size() * sizeof(float), hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(old.data(), pts_s(c), old.size() * sizeof(float), hipMemcpyDeviceToHost));
         c->sch_x_prev = x_coords(c->ns, old.data());
     }
     if (ns > 0) {
@@ -1602,9 +1627,9 @@ int iblb_get_lagrangian(iblb_ctx* c, float* s, float* u_s, int* epsilon) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     const size_t ns = (size_t)c->ns;
     if (ns == 0) return IBLB_OK;
-    if (s) HIP_TRY(c, hipMemcpy(s, c->d_s, 2 * ns * sizeof(float), hipMemcpyDeviceToHost));
-    if (u_s) HIP_TRY(c, hipMemcpy(u_s, c->d_us, 2 * ns * sizeof(float), hipMemcpyDeviceToHost));
-    if (epsilon) HIP_TRY(c, hipMemcpy(epsilon, c->d_eps, ns * sizeof(int), hipMemcpyDeviceToHost));
+    if (s) HIP_TRY(c, hipMemcpy(s, pts_s(c), 2 * ns * sizeof(float), hipMemcpyDeviceToHost));
+    if (u_s) HIP_TRY(c, hipMemcpy(u_s, pts_us(c), 2 * ns * sizeof(float), hipMemcpyDeviceToHost));
+    if (epsilon) HIP_TRY(c, hipMemcpy(epsilon, pts_eps(c), ns * sizeof(int), hipMemcpyDeviceToHost));
     return IBLB_OK;
 }
 
@@ -2146,9 +2171,10 @@ int iblb_save_checkpoint(iblb_ctx* c, const char* path) {
                           std::fwrite(dv, sizeof(dv), 1, fl.f) == 1);
     if (rc || (rc = ck_pops(c, fl, true))) return rc;
     const size_t ns = (size_t)c->ns;
-    if ((rc = ck_dev(c, fl, true, c->d_s, 2 * ns * sizeof(float))) ||
-        (rc = ck_dev(c, fl, true, c->d_us, 2 * ns * sizeof(float))) ||
-        (rc = ck_dev(c, fl, true, c->d_eps, ns * sizeof(int))))
+    // (under a schedule: the entry in use; the restart continues with those points)
+    if ((rc = ck_dev(c, fl, true, (void*)pts_s(c), 2 * ns * sizeof(float))) ||
+        (rc = ck_dev(c, fl, true, (void*)pts_us(c), 2 * ns * sizeof(float))) ||
+        (rc = ck_dev(c, fl, true, (void*)pts_eps(c), ns * sizeof(int))))
         return rc;
     if (c->cilia_on) {
         const size_t nk = (size_t)CILIA_SAMPLES * c->cilia.c_num;
@@ -2216,6 +2242,9 @@ int iblb_load_checkpoint(iblb_ctx* c, const char* path) {
         HIP_TRY(c, hipMemsetAsync(c->flags, 0, (size_t)c->ncol * c->nch, c->stream));
     }
     c->ns = (int)ns;
+    c->sch_n = 0;  // the restored points are static
+    c->sch_cur = -1;
+    c->band_sticky = false;
     c->band_valid = false;
     if (ns > 0 && !c->cilia_on) {  // the band plan of the restored points
         std::vector<float> hs(2 * ns);
