@@ -121,19 +121,23 @@ hipError_t launch_ib_point(const T* g, Layout L, Halo<T> H, int nx, int ns, cons
 // the same data in the same order, so the force is bit-identical to a single slab; F_s is
 // reported by the slab holding column min(x0, XDIM-1) (zeros elsewhere: the reader sums).
 // Needs the reference's invariant 0 <= nearbyint(xs) <= XDIM (boundary_check, main.cu:202-205).
+// part: 0 every point, 1 the inner points (x_begin+2 <= x0 <= x_begin+ncol-3: nodes and their
+// pulls inside the slab, no halo; they spread into columns >= 1 and <= ncol-2 only), 2 the others
+// (need the IB halo; they spread into columns <= 2 and >= ncol-3 only).
 template <typename T>
 __global__ __launch_bounds__(256) void ib_slab_kernel(const T* __restrict__ g, Layout L, IbHalo<T> X, int nx,
                                                       int x_begin, int ns, const float* __restrict__ s,
                                                       const float* __restrict__ u_s, const int* __restrict__ eps,
                                                       float* __restrict__ F_s, double* __restrict__ fd, long fplane,
-                                                      uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
+                                                      uint8_t* __restrict__ flags, int nch, int rows_per_chunk,
+                                                      int part) {
 #pragma clang fp contract(off)
     const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const int k = (int)(tid / LANES_PER_POINT), n = (int)(tid % LANES_PER_POINT);
     const bool pt = k < ns;
     float xs = 0.f, ys = 0.f;
     int x0 = 0, x = 0, y = 0;
-    bool mine = false;
+    bool mine = false, fs_here = true;  // fs_here: this launch writes the point's F_s entry
     if (pt) {
         xs = s[2 * k + 0];
         ys = s[2 * k + 1];
@@ -141,6 +145,12 @@ __global__ __launch_bounds__(256) void ib_slab_kernel(const T* __restrict__ g, L
         for (int dx = -1; dx <= 1; ++dx) {  // group-uniform: does the point spread into this slab?
             const int xx = x0 + dx;
             mine |= xx >= 0 && xx < nx && xx >= x_begin && xx < x_begin + L.ncol;
+        }
+        const bool inner = x0 >= x_begin + 2 && x0 <= x_begin + L.ncol - 3;
+        if (part == 1) fs_here = mine = mine && inner;
+        if (part == 2) {
+            fs_here = !(mine && inner);  // the edge launch also zeroes the points of other slabs
+            mine = mine && !inner;
         }
     }
     double tx = 0., ty = 0.;
@@ -171,7 +181,7 @@ __global__ __launch_bounds__(256) void ib_slab_kernel(const T* __restrict__ g, L
     float Fx, Fy;
     fold_terms(tx, ty, valid, Fx, Fy);
     if (!pt || n >= 9) return;
-    if (n == 0) {
+    if (n == 0 && fs_here) {
         const int xo = x0 < nx - 1 ? x0 : nx - 1;
         const bool owner = xo >= x_begin && xo < x_begin + L.ncol;
         F_s[2 * k + 0] = owner ? Fx : 0.f;
@@ -183,11 +193,11 @@ __global__ __launch_bounds__(256) void ib_slab_kernel(const T* __restrict__ g, L
 template <typename T>
 hipError_t launch_ib_slab(const T* g, Layout L, IbHalo<T> X, int nx, int x_begin, int ns, const float* s,
                           const float* u_s, const int* eps, float* F_s, double* fdense, long fplane, uint8_t* flags,
-                          int nch, int rows_per_chunk, hipStream_t st) {
+                          int nch, int rows_per_chunk, hipStream_t st, int part) {
     if (ns <= 0) return hipSuccess;
     const long n = (long)LANES_PER_POINT * ns;
     ib_slab_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(g, L, X, nx, x_begin, ns, s, u_s, eps, F_s, fdense,
-                                                                    fplane, flags, nch, rows_per_chunk);
+                                                                    fplane, flags, nch, rows_per_chunk, part);
     return hipGetLastError();
 }
 
@@ -214,10 +224,10 @@ hipError_t launch_pack_ib_halo(const T* g, Layout L, T* send_left, T* send_right
 
 template hipError_t launch_ib_slab<double>(const double*, Layout, IbHalo<double>, int, int, int, const float*,
                                            const float*, const int*, float*, double*, long, uint8_t*, int, int,
-                                           hipStream_t);
+                                           hipStream_t, int);
 template hipError_t launch_ib_slab<float>(const float*, Layout, IbHalo<float>, int, int, int, const float*,
                                           const float*, const int*, float*, double*, long, uint8_t*, int, int,
-                                          hipStream_t);
+                                          hipStream_t, int);
 template hipError_t launch_pack_ib_halo<double>(const double*, Layout, double*, double*, hipStream_t);
 template hipError_t launch_pack_ib_halo<float>(const float*, Layout, float*, float*, hipStream_t);
 template hipError_t launch_ib_point<double>(const double*, Layout, Halo<double>, int, int, const float*, const float*,

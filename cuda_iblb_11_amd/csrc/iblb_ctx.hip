@@ -524,6 +524,42 @@ int overlapped_step(iblb_ctx* c) {
     return IBLB_OK;
 }
 
+// RCCL slab with an IB force owed (force^t of the points of iteration t-1), step t on two streams:
+//   compute: (join_comm: boundary(t-1)) -> IB of the inner points -> ev_pre -> interior columns
+//            [3, ncol-3)(t) -> ev_int
+//   comm:    wait int(t-1) -> IB halo pack + exchange(t) -> IB of the edge points -> wait ev_pre ->
+//            boundary columns [0, 3) and [ncol-3, ncol)(t) -> ev_bnd
+// Inner points (x_begin+2 <= x0 <= x_begin+ncol-3: nodes and pulls inside the slab) need no halo
+// and spread into columns [1, ncol-2]; edge points need the IB halo and spread into columns
+// <= 2 and >= ncol-3 only, so the interior collide waits for neither the exchange nor the edge
+// IB.  boundary(t) waits for the inner IB (its columns 1, 2 / ncol-3, ncol-2 may hold inner
+// forces) and for interior(t-1) (which read the columns it overwrites); interior(t) and the
+// inner IB of t read columns boundary(t-1) wrote (join_comm).  next: the schedule entry the
+// iteration's points switch to after the owed force is evaluated (-1: unchanged).
+template <typename T>
+int ib_overlapped_step(iblb_ctx* c, int next) {
+    hipStream_t bs = c->comm_stream;
+    IbHalo<T> X{(const T*)c->recv_left, (const T*)c->recv_right};
+    int rc;
+    HIP_TRY(c, launch_ib_slab<T>(gptr<T>(c, c->cur), c->L, X, c->nx, c->x_begin, c->ns, pts_s(c), pts_us(c), pts_eps(c),
+                                 c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream, 1));
+    HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
+    HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
+    if ((rc = exchange_rccl(c, bs, true))) return rc;
+    HIP_TRY(c, launch_ib_slab<T>(gptr<T>(c, c->cur), c->L, X, c->nx, c->x_begin, c->ns, pts_s(c), pts_us(c), pts_eps(c),
+                                 c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, bs, 2));
+    c->ib_state = IB_READY;
+    if (next >= 0 && (rc = sched_use(c, next))) return rc;
+    HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_pre, 0));
+    if ((rc = launch_fused_step<T>(c, 0, 3, 1, false, bs))) return rc;
+    if ((rc = launch_fused_step<T>(c, c->ncol - 3, 3, 1, false, bs))) return rc;
+    HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
+    if ((rc = launch_fused_step<T>(c, 3, c->ncol - 6))) return rc;
+    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+    after_step(c);
+    return IBLB_OK;
+}
+
 // Compute stream after the boundary columns of the current state (they may have been written
 // on the comm stream by an overlapped step).
 int join_comm(iblb_ctx* c) {
@@ -914,6 +950,10 @@ int step_one(iblb_ctx* c) {
             if ((rc = ensure_force(c))) return rc;
         }
         if ((rc = run_cilia(c))) return rc;
+    } else if (c->phase == PH_RUN && rccl_multi(c) && c->overlap && c->ib_state == IB_PENDING && !c->halo_valid &&
+               c->ncol >= 9 && env_long("IBLB_IB_OVERLAP", 1)) {
+        const int next = c->sch_n > 0 && sched_entry(c, c->t) != c->sch_cur ? sched_entry(c, c->t) : -1;
+        return c->prec == IBLB_PREC_F64 ? ib_overlapped_step<double>(c, next) : ib_overlapped_step<float>(c, next);
     } else if (c->sch_n > 0 && sched_entry(c, c->t) != c->sch_cur) {
         // the force owed to the previous iteration's points first, then this iteration's points
         if (c->phase == PH_RUN) {

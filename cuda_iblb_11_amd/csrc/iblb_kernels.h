@@ -150,11 +150,12 @@ template <typename T>
 hipError_t launch_ib_point(const T* g, Layout L, Halo<T> H, int nx, int ns, const float* s, const float* u_s,
                            const int* eps, float* F_s, double* fdense, long fplane, uint8_t* flags, int nch,
                            int rows_per_chunk, hipStream_t st);
-// Slab groups: the points spreading into this slab, nodes pulled through the IB halo.
+// Slab groups: the points spreading into this slab, nodes pulled through the IB halo.  part: 0
+// all, 1 inner points only (no halo needed), 2 the points near the slab edges.
 template <typename T>
 hipError_t launch_ib_slab(const T* g, Layout L, IbHalo<T> X, int nx, int x_begin, int ns, const float* s,
                           const float* u_s, const int* eps, float* F_s, double* fdense, long fplane, uint8_t* flags,
-                          int nch, int rows_per_chunk, hipStream_t st);
+                          int nch, int rows_per_chunk, hipStream_t st, int part = 0);
 // IB halo slots 3.. of both send buffers from the state g.
 template <typename T>
 hipError_t launch_pack_ib_halo(const T* g, Layout L, T* send_left, T* send_right, hipStream_t st);

@@ -34,11 +34,14 @@ def main():
     bf = (1e-6, 2e-7)
     edge = plan_slabs(nx, n)[0][1] - 0.4  # filament straddling the slab 0 | slab 1 edge
 
+    mid = plan_slabs(nx, n)[0][1] / 2 + 0.2  # inner points of slab 0 (IB without the halo)
+
     def pts(it):  # plus one at x = XDIM (nodes wrap to column 0 of the next row)
         a = W.filament(it, n_points=40, x0=edge, y0=1.0, U0=2e-3, period=30, sway=2.0)
         b = W.filament(it, n_points=20, x0=nx - 0.3, y0=50.0, U0=2e-3, period=30, sway=0.5)
-        return tuple(np.concatenate([p, q]) for p, q in zip(a, b))
-    mp = 64 if with_ib else 0
+        c = W.filament(it, n_points=16, x0=mid, y0=80.0, U0=2e-3, period=30, sway=1.0)
+        return tuple(np.concatenate([p, q, r]) for p, q, r in zip(a, b, c))
+    mp = 96 if with_ib else 0
 
     single = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, lib=lib)
     single.set_state(rho, u)

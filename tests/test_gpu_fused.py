@@ -391,8 +391,11 @@ def test_rccl_self_ring(gpu, monkeypatch, overlap, reserve, with_ib):
     monkeypatch.setenv("IBLB_RESERVE_CUS", str(reserve))
     nx, ny, steps = 96, 200, 30
     rho, u = W.perturbed_state(nx, ny, 5)
-    pts = lambda it: W.filament(it, n_points=40, x0=nx - 0.6, y0=1.0, U0=2e-3, period=30, sway=2.0)
-    kw = dict(body_force=(1e-6, 2e-7), max_points=64 if with_ib else 0)
+    def pts(it):  # points at the slab edge (IB halo) and inside it (no halo)
+        a = W.filament(it, n_points=40, x0=nx - 0.6, y0=1.0, U0=2e-3, period=30, sway=2.0)
+        b = W.filament(it, n_points=30, x0=40.3, y0=20.0, U0=2e-3, period=30, sway=2.0)
+        return tuple(np.concatenate([p, q]) for p, q in zip(a, b))
+    kw = dict(body_force=(1e-6, 2e-7), max_points=80 if with_ib else 0)
     ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)
     ring = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)
     ref.set_state(rho, u)
