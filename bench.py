@@ -55,8 +55,9 @@ def workload_points(kind, nx):
     from cuda_iblb_11_amd import workloads as W
     if kind == "filament":
         return lambda it: W.filament(it, n_points=256, x0=nx / 2 + 0.3, y0=1.0, dy=1.0, U0=1e-3, period=1000)
-    if kind == "array":
-        return lambda it: W.filament_array(it, nx, n_fil=64, pts=96, period=1000)
+    if kind == "array":  # 64 filaments per 8192 columns (a K5 slab of 1024 columns holds 8)
+        nf = max(1, round(64 * nx / 8192))
+        return lambda it: W.filament_array(it, nx, n_fil=nf, pts=96, period=1000)
     return None
 
 

@@ -735,9 +735,14 @@ int sweepk_step(iblb_ctx* c) {
 // columns of g^{t+K}; each column is collided by the same kernels as one-step iterations, so the
 // result equals K one-step iterations (the deep sweep is bit-identical to them, the trapezoid
 // runs the one-step kernels themselves).
+// the band cycle's geometry: a lone slab, or a slab of an RCCL group whose bands stay in its
+// interior (the boundary columns then advance force-free from the deep halo, as deep_slab_step)
+bool band_slab_ok(const iblb_ctx* c) {
+    return rccl_multi(c) && c->overlap && c->comm_stream && c->ncol >= 4 * c->sweep_depth;
+}
 bool band_ready(const iblb_ctx* c) {
-    return c->band_on && c->band_valid && single_slab(c) && c->phase == PH_RUN && !c->cilia_on && ib_active(c) &&
-           c->sweep_on && c->sweep_depth >= 3;
+    return c->band_on && c->band_valid && (single_slab(c) || band_slab_ok(c)) && c->phase == PH_RUN &&
+           !c->cilia_on && ib_active(c) && c->sweep_on && c->sweep_depth >= 3;
 }
 
 template <typename T>
@@ -751,18 +756,43 @@ int band_step(iblb_ctx* c) {
     // band chain on band_st (the reserved XCDs).  The context's own stream keeps the whole chip
     // (iblb_get_stream hands it out; every other step runs on it): the two masked streams start
     // after its work so far, and it waits for both at the end of the cycle.
-    const bool ov = c->band_st != nullptr;
+    //
+    // A slab of an RCCL group (bands in its interior, every point's trapezoid inside its slab):
+    // the compute stream runs the IB, the gaps' deep sweep and the band chain on interior columns
+    // (none reads the halo); the comm stream exchanges the deep halo and advances the force-free
+    // boundary columns [0, K), [ncol-K, ncol) exactly as deep_slab_step does.
+    const bool slab = !single_slab(c);
+    const bool ov = c->band_st != nullptr && !slab;
     hipStream_t bs = ov ? c->band_st : c->stream, ds = ov ? c->deep_st : c->stream;
+    if (slab) {
+        if ((rc = join_comm(c))) return rc;  // boundary(t-K) wrote columns the interior reads
+        if (c->send_deep != K) {            // the send buffers hold another halo: pack the deep one
+            HIP_TRY(c, launch_pack_deep_halo<T>(A, c->L, K, (T*)c->send_left, (T*)c->send_right, c->stream));
+            HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+            HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+            HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+        }
+        HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
+    }
     if (ov) {
         HIP_TRY(c, hipEventRecord(c->ev_b0, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_b0, 0));
         HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_b0, 0));
     }
+    // IB of one level: a lone slab with every point; a group slab with the points spreading into
+    // it (all inner: no halo is read) and zero F_s for the others
+    IbHalo<T> X{(const T*)c->recv_left, (const T*)c->recv_right};
+    auto ib = [&](const T* g, const float* ps, const float* pus, const int* pe, hipStream_t st) -> hipError_t {
+        if (!slab)
+            return launch_ib_point<T>(g, c->L, halo_at<T>(c, g), c->nx, c->ns, ps, pus, pe, c->d_Fs, c->fdense, c->fplane,
+                                      c->flags, c->nch, 64 * c->V, st);
+        return launch_ib_slab<T>(g, c->L, X, c->nx, c->x_begin, c->ns, ps, pus, pe, c->d_Fs, c->fdense, c->fplane,
+                                 c->flags, c->nch, 64 * c->V, st, 0);
+    };
     if (c->ib_state == IB_PENDING) {  // force^t from g^t
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, bs))) return rc;
-        HIP_TRY(c, launch_ib_point<T>(A, c->L, halo_at<T>(c, A), c->nx, c->ns, pts_s(c), pts_us(c), pts_eps(c), c->d_Fs,
-                                      c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, bs));
+        HIP_TRY(c, ib(A, pts_s(c), pts_us(c), pts_eps(c), bs));
         if ((rc = ev_end(c, ev, EV_IB, 0, bs))) return rc;
         c->ib_state = IB_READY;
     }
@@ -775,6 +805,8 @@ int band_step(iblb_ctx* c) {
         if (d.map == 0) d.map = 2;
         const int per_xcd = std::max(1, c->ncu / 8);
         if (ov && c->band_reserve % per_xcd == 0) d.xcds = 8 - c->band_reserve / per_xcd;
+        if (slab && c->reserved_cus % per_xcd == 0 && env_long("IBLB_DEEP_XCD_DEAL", 1))
+            d.xcds = 8 - c->reserved_cus / per_xcd;  // the compute stream leaves whole XCDs to the comm stream
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, ds))) return rc;
         HIP_TRY(c, launch_sweepk<T>(d, K, false, ds));
@@ -795,8 +827,7 @@ int band_step(iblb_ctx* c) {
             }
             size_t ev = 0;
             if ((rc = ev_begin(c, &ev, bs))) return rc;
-            HIP_TRY(c, launch_ib_point<T>(src, c->L, halo_at<T>(c, src), c->nx, c->ns, ps, pus, pe, c->d_Fs, c->fdense,
-                                          c->fplane, c->flags, c->nch, 64 * c->V, bs));
+            HIP_TRY(c, ib(src, ps, pus, pe, bs));
             if ((rc = ev_end(c, ev, EV_IB, 0, bs))) return rc;
         }
         FusedArgs<T> a;
@@ -829,6 +860,23 @@ int band_step(iblb_ctx* c) {
         HIP_TRY(c, hipEventRecord(c->ev_b2, bs));
         HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b1, 0));
         HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b2, 0));
+    }
+    if (slab) {
+        // comm: deep halo exchange(t) -> (after the compute work before this cycle, which read
+        // the columns the boundary sweeps overwrite) boundary sweeps -> deep halo of g^{t+K}
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        hipStream_t cs = c->comm_stream;
+        if ((rc = exchange_rccl(c, cs, false, false, deep_slots(K)))) return rc;
+        HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_pre, 0));
+        Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
+        b.vs = c->deep_bnd_vs;
+        b.variant = c->deep_variant;
+        if (b.map == 0) b.map = 2;
+        HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));
+        HIP_TRY(c, launch_pack_deep_halo<T>(B, c->L, K, (T*)c->send_left, (T*)c->send_right, cs));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));
+        c->send_sweep = false;
+        c->send_deep = K;
     }
     c->cur = 1 - c->cur;
     c->t += K;
@@ -1356,12 +1404,29 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
 // the lattice, bands within 2(K-1) columns of the lattice edge: the reference's flat-index wrap).
 template <typename T>
 static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
-    const int K = c->sweep_depth, nx = c->nx, R = 2 * (K - 1);
+    const int K = c->sweep_depth, R = 2 * (K - 1);
+    // A slab of an RCCL group: local columns, bands and gaps inside [K, ncol-K).  Every rank
+    // holds every point and tests every point against its own slab's interior, so all ranks take
+    // the same decision (the cycle's deep-halo exchange is collective).
+    const bool slab = !single_slab(c);
+    const int nx = slab ? c->ncol : c->nx;  // local columns
+    const int lo = slab ? K : 0, hi = slab ? c->ncol - K : c->nx;
     // forced columns [x0-1, x0+1] of every point, as a column mask
     std::vector<char> forced((size_t)nx, 0);
     for (float xv : xs) {
-        const double x0 = std::nearbyint((double)xv);
-        if (!(x0 - 1 - R >= 0. && x0 + 1 + R <= nx - 1.)) {
+        double x0 = std::nearbyint((double)xv);
+        if (slab) {
+            int r = -1;
+            for (size_t q = 0; q < c->slab_begin.size(); ++q)
+                if (x0 >= c->slab_begin[q] && x0 < c->slab_begin[q] + c->slab_count[q]) r = (int)q;
+            const double b = r >= 0 ? c->slab_begin[(size_t)r] : 0., e = r >= 0 ? b + c->slab_count[(size_t)r] : 0.;
+            if (r < 0 || !(x0 - 1 - R >= b + K && x0 + 1 + R <= e - 1 - K)) {
+                c->band_valid = false;
+                return IBLB_OK;
+            }
+            if (r != c->rank) continue;
+            x0 -= c->x_begin;
+        } else if (!(x0 - 1 - R >= 0. && x0 + 1 + R <= nx - 1.)) {
             c->band_valid = false;
             return IBLB_OK;
         }
@@ -1393,15 +1458,15 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
         cnt[j] = (int)tab.size() - off[j];
         cols += cnt[j];
     }
-    if (2 * cols > (long long)K * nx) return IBLB_OK;
+    if (!slab && 2 * cols > (long long)K * nx) return IBLB_OK;  // (a slab: the same decision on every rank)
     // the gaps: columns farther than K-1 from every forced column
     std::vector<std::pair<int, int>> gaps;
-    int prev = 0;
+    int prev = lo;
     for (auto& iv : b) {
         if (iv.first - (K - 1) > prev) gaps.push_back({prev, iv.first - (K - 1)});
         prev = iv.second + K;
     }
-    if (prev < nx) gaps.push_back({prev, nx});
+    if (prev < hi) gaps.push_back({prev, hi});
     long long ndeep = 0;
     for (auto& g : gaps) ndeep += g.second - g.first;
     int rc = band_streams(c, cols, ndeep);
@@ -1411,7 +1476,7 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
     const int W = std::max(1, c->deep_w);
     int nch = 0;
     const int wpc = sweepk_geometry<T>(K, c->deep_vs, c->deep_variant, false, c->ny, &nch);
-    const int ncu = c->ncu - c->band_reserve;
+    const int ncu = (slab ? c->ncu - c->reserved_cus : c->ncu - c->band_reserve);
     long nsw = (long)((ndeep + W - 1) / W);
     const long slots = (long)wpc * ncu;
     if (c->deep_balance && slots > 0 && nch > 0 && ndeep > 0) {
@@ -1476,7 +1541,7 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
     c->band_deep_cols = ndeep;
     c->band_cols = cols;
     c->band_flux = -1;
-    const int fc = c->cfg.flux_column;
+    const int fc = c->cfg.flux_column - (slab ? c->x_begin : 0);
     for (auto& iv : b)
         if (fc >= iv.first - (K - 1) && fc <= iv.second + (K - 1)) c->band_flux = fc;
     c->band_b = b;
@@ -1485,7 +1550,8 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
 }
 
 static int plan_bands(iblb_ctx* c, const std::vector<float>& xs) {
-    if (!c->band_on || xs.empty() || c->sweep_depth < 3 || !c->sweep_on || c->ncol != c->nx || c->cilia_on) {
+    if (!c->band_on || xs.empty() || c->sweep_depth < 3 || !c->sweep_on || !(single_slab(c) || band_slab_ok(c)) ||
+        c->cilia_on) {
         c->band_valid = false;
         return IBLB_OK;
     }

@@ -27,8 +27,11 @@ from cuda_iblb_11_amd.lattice import Lattice, plan_slabs, rccl_unique_id, split_
 
 def main():
     n, nx, ny, steps, with_ib, prec = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]),
-                                        sys.argv[5] == "1", sys.argv[6])
-    bulk = len(sys.argv) > 7 and sys.argv[7] == "1" and not with_ib
+                                        sys.argv[5] in ("1", "2"), sys.argv[6])
+    # IB mode "2": one filament moving inside each slab, points given ahead (iblb_set_lagrangian_steps)
+    # and stepped in bulk: the IB band cycle of slab groups
+    band = sys.argv[5] == "2"
+    bulk = len(sys.argv) > 7 and sys.argv[7] == "1" and (not with_ib or band)
     lib = L.load_from(os.path.join(HERE, "libiblb_mockrccl.so"))
     rho, u = W.perturbed_state(nx, ny, 31)
     bf = (1e-6, 2e-7)
@@ -42,6 +45,18 @@ def main():
         c = W.filament(it, n_points=16, x0=mid, y0=80.0, U0=2e-3, period=30, sway=1.0)
         return tuple(np.concatenate([p, q, r]) for p, q, r in zip(a, b, c))
     mp = 96 if with_ib else 0
+    if band:
+        def pts(it):
+            parts = []
+            for xb_, xc_ in plan_slabs(nx, n):
+                ph = 2 * np.pi * it / 20
+                parts.append(W.filament(it, n_points=12, x0=xb_ + xc_ / 2 + 0.3 + np.sin(ph), y0=10.0, U0=2e-3,
+                                        period=20, sway=0.8))
+            return tuple(np.concatenate(q) for q in zip(*parts))
+
+    def sched(t0, k):
+        e = [pts(it) for it in range(t0, t0 + k)]
+        return np.stack([x[0] for x in e]), np.stack([x[1] for x in e]), np.stack([x[2] for x in e])
 
     single = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, lib=lib)
     single.set_state(rho, u)
@@ -49,6 +64,7 @@ def main():
         if with_ib:
             single.set_lagrangian(*pts(it))
         single.step(1)
+    # (mode 2: the reference run takes the points per iteration, the slabs get them ahead)
     r1, u1 = single.macro()
     q1 = single.flux
     f1 = single.lagrangian_force() if with_ib else None
@@ -79,6 +95,9 @@ def main():
                       x_count=xc, lib=lib)
         lat.set_state(split_state(rho, 1, nx, ny, xb, xc), split_state(u, 2, nx, ny, xb, xc))
         lat.attach_rccl(uid, n, r)
+        if band:
+            lat.set_lagrangian_steps(*sched(0, steps))
+            lat.set_profiling(True)
         if bulk:  # calls of 3, 1, 2, ... steps up to the checkpoint, the rest in one call
             t = 0
             for k in (3, 1, 2, 4):
@@ -94,6 +113,8 @@ def main():
             if with_ib:
                 lat.set_lagrangian(*pts(it))
             lat.step(1)
+        if band and lat.timing()["sweepk_launches"] == 0:
+            raise RuntimeError("the band cycle did not run")
         rs, us = lat.macro()
         out[r] = (xb, xc, rs, us, lat.flux, lat.lagrangian_force() if with_ib else None)  # collective
         gathered[r] = lat.gather_macro(0)  # collective output gather to rank 0
@@ -108,6 +129,8 @@ def main():
                       x_count=xc, lib=lib)
         lat.attach_rccl(uid2, n, r)
         lat.load_checkpoint(ck(r))
+        if band:  # the checkpoint holds the points of iteration half-1; the rest given ahead again
+            lat.set_lagrangian_steps(*sched(half, steps - half))
         if bulk:
             lat.step(steps - half)
         for it in range(half if not bulk else steps, steps):

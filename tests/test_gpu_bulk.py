@@ -262,3 +262,35 @@ def test_band_streams_keep_the_context_stream(gpu, monkeypatch):
     r1, u1 = lat.macro()
     r2, u2 = ref2.macro()
     assert rel(r1, r2) <= 1e-13 and rel(u1, u2) <= 1e-12
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_rccl_self_ring_ib_band_cycle(gpu, monkeypatch, precision):
+    """The IB band cycle of a slab group over REAL RCCL (one rank, its own neighbour): moving
+    filaments inside the slab, points given ahead, bulk calls with readers between them; equals
+    the lone slab (same band cycle without halos) up to the spread atomics' order."""
+    from cuda_iblb_11_amd import workloads as W
+    monkeypatch.setenv("IBLB_RCCL_SELF", "1")
+    nx, ny = 256, 128
+    pts = _swaying(nx, n_fil=2, pts=40)
+    rho, u = W.perturbed_state(nx, ny, 17)
+    kw = dict(precision=precision, body_force=(1e-6, 0.0), max_points=80)
+    ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)
+    ring = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)
+    ref.set_state(rho, u)
+    ring.set_state(rho, u)
+    ring.attach_rccl(gpu.rccl_unique_id(), 1, 0)
+    ring.set_profiling(True)
+    t = 0
+    for n in (1, 12, 7, 10):
+        for lat in (ref, ring):
+            lat.set_lagrangian_steps(*_schedule(pts, t, n))
+            lat.step(n)
+        t += n
+        r1, u1 = ref.macro()
+        r2, u2 = ring.macro()
+        tol = 1e-12 if precision == "f64" else 1e-5
+        assert rel(r2, r1) <= tol and rel(u2, u1) <= tol, n
+    assert ring.timing()["sweepk_launches"] >= 4
+    assert abs(ring.flux - ref.flux) <= 1e-11 * abs(ref.flux)
+    ring.close()

@@ -270,7 +270,7 @@ def test_errors_are_loud(gpu):
                           (2, False, "f64", 1, 1, 5), (3, False, "f64", 1, 1, 5), (3, False, "f64", 0, 1, 5),
                           (4, False, "f32", 1, 1, 5), (2, False, "f64", 1, 1, 2), (3, False, "f32", 1, 1, 2),
                           (3, False, "f64", 1, 1, 3), (4, False, "f64", 1, 1, 6)])
-def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap, bulk, depth):
+def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap, bulk, depth, nx=48):
     """The RCCL transport of iblb_ctx.hip (attach, halo send/recv pairing, node-value and
     flux all-reduces, collective readers) driven with N ranks as threads on the one GPU via
     the mock-RCCL test build (RCCL itself refuses two ranks on one device).  Without IB the
@@ -282,14 +282,23 @@ def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap, bulk, depth
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    cmd = [sys.executable, os.path.join(here, "mock_rccl", "run_group.py"), str(n), "48", "130", "25",
-           "1" if with_ib else "0", precision, str(bulk)]
+    ib = {False: "0", True: "1"}.get(with_ib, with_ib)  # "2": interior filaments, band cycle
+    cmd = [sys.executable, os.path.join(here, "mock_rccl", "run_group.py"), str(n), str(nx), "130", "25", ib,
+           precision, str(bulk)]
     env = dict(os.environ, IBLB_OVERLAP=str(overlap), IBLB_SWEEP_DEPTH=str(depth))
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert lines, p.stdout + p.stderr
     res = json.loads(lines[-1])
     assert p.returncode == 0 and res["ok"], (res, p.stderr[-2000:])
+
+
+@pytest.mark.parametrize("n,precision", [(2, "f64"), (3, "f32"), (4, "f64")])
+def test_rccl_slab_band_cycle_threads(gpu, n, precision):
+    """The IB band cycle on a slab group (mock RCCL, ranks as threads): one filament moving inside
+    each slab, points given ahead, bulk steps and a checkpoint restart; must equal the single slab
+    stepped one iteration at a time up to the spread atomics' order."""
+    test_rccl_slab_path_threads(gpu, n, "2", precision, 1, 1, 5, nx=48 * n)
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
