@@ -23,6 +23,9 @@
 #include <vector>
 
 #include "../../include/iblb.h"
+
+// defined only by the tests' in-process RCCL stand-in (tests/mock_rccl/mock_rccl.cpp)
+extern "C" __attribute__((weak)) int iblb_mock_rccl(void);
 #include "cilia_kernels.h"
 #include "iblb_kernels.h"
 
@@ -160,6 +163,14 @@ struct iblb_ctx {
     hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with the interior
     hipEvent_t ev_bnd = nullptr;  // boundary columns + send buffers of the state written (either stream)
     hipEvent_t ev_int = nullptr;  // compute-stream work of the last step done
+    unsigned* d_sig = nullptr;    // deep slab cycle: [0] boundary signal, [1] wait timeout flag,
+                                  // [2] boundary waves done (counter of the running launch)
+    unsigned sig_seq = 0;         // value the last boundary sweep released
+    unsigned edge_seq = 0;        // value the last interior's edge sweeps release ([3], counter [4])
+    bool edge_last = false;       // ... and that interior was the last compute work of a deep cycle
+    bool int_stale = false;       // ev_int not recorded after the last deep cycle's interior
+    bool sig_last = false;        // ev_bnd's last record followed that signal (nothing else since)
+    bool slab_signal = false;     // IBLB_SLAB_SIGNAL: interiors wait on d_sig instead of ev_bnd
     hipEvent_t ev_pre = nullptr;  // compute-stream work before the interior sweep (sweep order 1)
     bool overlap = true;
     int sweep_order = 0;          // IBLB_SWEEP_ORDER: 1 = the host submits the interior sweep first
@@ -323,6 +334,29 @@ int ev_end(iblb_ctx* c, size_t idx, int kind, long long cells = 0, hipStream_t s
 }
 
 // ---- halo exchange ----------------------------------------------------------------------
+// ev_bnd marks "boundary columns and send buffers of the current state written"; a record by
+// anything but the deep slab cycle's signal path ends that path's device-side signal chain.
+static hipError_t rec_bnd(iblb_ctx* c, hipStream_t st) {
+    c->sig_last = false;
+    return hipEventRecord(c->ev_bnd, st);
+}
+static hipError_t rec_int(iblb_ctx* c) {
+    c->int_stale = false;
+    c->edge_last = false;
+    return hipEventRecord(c->ev_int, c->stream);
+}
+// st after the compute work of the last step (ev_int; the deep cycle's signal path leaves it to be
+// recorded here, on demand: a later record on the compute stream covers the same work and more)
+static hipError_t wait_int(iblb_ctx* c, hipStream_t st) {
+    c->edge_last = false;  // another step follows
+    if (c->int_stale) {
+        hipError_t e = hipEventRecord(c->ev_int, c->stream);
+        if (e != hipSuccess) return e;
+        c->int_stale = false;
+    }
+    return hipStreamWaitEvent(st, c->ev_int, 0);
+}
+
 // IB slots of the send buffers (slots 0-2 come from the collide)
 template <typename T>
 int pack_ib(iblb_ctx* c, hipStream_t st) {
@@ -385,8 +419,8 @@ int pack_send(iblb_ctx* c) {
     c->send_sweep = false;
     c->send_deep = 0;
     if (rccl_multi(c)) {
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, rec_bnd(c, c->stream));
+        HIP_TRY(c, rec_int(c));
         HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     return IBLB_OK;
@@ -515,11 +549,11 @@ template <typename T>
 int overlapped_step(iblb_ctx* c) {
     int rc = exchange_rccl(c, c->comm_stream);
     if (rc) return rc;
-    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_int, 0));
+    HIP_TRY(c, wait_int(c, c->comm_stream));
     if ((rc = launch_fused_step<T>(c, 0, 2, c->ncol - 1, false, c->comm_stream))) return rc;
-    HIP_TRY(c, hipEventRecord(c->ev_bnd, c->comm_stream));
+    HIP_TRY(c, rec_bnd(c, c->comm_stream));
     if ((rc = launch_fused_step<T>(c, 1, c->ncol - 2))) return rc;
-    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+    HIP_TRY(c, rec_int(c));
     after_step(c);
     return IBLB_OK;
 }
@@ -544,7 +578,7 @@ int ib_overlapped_step(iblb_ctx* c, int next) {
     HIP_TRY(c, launch_ib_slab<T>(gptr<T>(c, c->cur), c->L, X, c->nx, c->x_begin, c->ns, pts_s(c), pts_us(c), pts_eps(c),
                                  c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream, 1));
     HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
-    HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
+    HIP_TRY(c, wait_int(c, bs));
     if ((rc = exchange_rccl(c, bs, true))) return rc;
     HIP_TRY(c, launch_ib_slab<T>(gptr<T>(c, c->cur), c->L, X, c->nx, c->x_begin, c->ns, pts_s(c), pts_us(c), pts_eps(c),
                                  c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, bs, 2));
@@ -553,9 +587,9 @@ int ib_overlapped_step(iblb_ctx* c, int next) {
     HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_pre, 0));
     if ((rc = launch_fused_step<T>(c, 0, 3, 1, false, bs))) return rc;
     if ((rc = launch_fused_step<T>(c, c->ncol - 3, 3, 1, false, bs))) return rc;
-    HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
+    HIP_TRY(c, rec_bnd(c, bs));
     if ((rc = launch_fused_step<T>(c, 3, c->ncol - 6))) return rc;
-    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+    HIP_TRY(c, rec_int(c));
     after_step(c);
     return IBLB_OK;
 }
@@ -633,16 +667,23 @@ template <typename T>
 int deep_slab_step(iblb_ctx* c) {
     const int K = c->sweep_depth;
     const int W = std::max(1, c->deep_w);
-    int rc = join_comm(c);
+    const bool ov = c->overlap;
+    // signal path: the previous cycle's boundary released d_sig; the interior waits for it on the
+    // device (slab_wait) and the compute stream carries no cross-stream wait
+    const bool sig_path = ov && c->deep_order == 1 && c->slab_signal;
+    const bool sig_wait = sig_path && c->sig_last && c->send_deep == K;
+    // ... and the boundary waits for the previous interior's edge sweeps, not for all of it
+    const bool edge_wait = sig_wait && c->edge_last;
+    const unsigned edge_prev = c->edge_seq;
+    int rc = sig_wait ? IBLB_OK : join_comm(c);
     if (rc) return rc;
     if (c->send_deep != K) {  // the send buffers hold another halo: pack the deep one now
         HIP_TRY(c, launch_pack_deep_halo<T>(gptr<T>(c, c->cur), c->L, K, (T*)c->send_left, (T*)c->send_right,
                                             c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, rec_bnd(c, c->stream));
+        HIP_TRY(c, rec_int(c));
         HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
-    const bool ov = c->overlap;
     hipStream_t bs = ov ? c->comm_stream : c->stream;
     const int ni = c->ncol - 2 * K;  // interior [K, ncol-K): needs nothing from the halo
     auto interior = [&]() -> int {
@@ -650,12 +691,22 @@ int deep_slab_step(iblb_ctx* c) {
         Sweep2Args<T> a = sweep_args<T>(c, K, c->deep_balance ? 0 : W, c->ncol - K, (ni + W - 1) / W, W);
         a.vs = c->deep_slab_vs;
         a.cus = c->ncu - c->reserved_cus;  // the compute stream's CU mask
-        // whole XCDs reserved: the workgroups are dealt over the remaining ones
-        const int per_xcd = std::max(1, c->ncu / 8);
-        if (c->reserved_cus % per_xcd == 0 && env_long("IBLB_DEEP_XCD_DEAL", 1))
-            a.xcds = 8 - c->reserved_cus / per_xcd;
+        // the workgroups still go round-robin to all eight XCDs (mask bit i is a CU of XCD i % 8,
+        // profiles/r02n_xcc_probe.txt), so the XCD-contiguous deal stays over eight
+        a.xcds = (int)env_long("IBLB_DEEP_XCDS", 0);
         a.variant = c->deep_variant;
         if (a.map == 0) a.map = 2;
+        if (sig_wait) {
+            a.wait_sig = c->d_sig;
+            a.wait_val = c->sig_seq;
+            a.sig_err = c->d_sig + 1;
+        }
+        if (sig_path) {  // its first and last sweeps (edge_w columns) release the edge signal
+            a.edge_w = std::max(K, (int)env_long("IBLB_DEEP_EDGE_W", K));
+            a.sig_out = c->d_sig + 3;
+            a.done_ctr = c->d_sig + 4;
+            a.sig_val = ++c->edge_seq;
+        }
         size_t ev = 0;
         int r = ev_begin(c, &ev, c->stream);
         if (r) return r;
@@ -667,32 +718,47 @@ int deep_slab_step(iblb_ctx* c) {
         b.vs = c->deep_bnd_vs;
         b.variant = c->deep_variant;
         if (b.map == 0) b.map = 2;
+        if (sig_path) {  // its last wave releases the signal the next interior waits for
+            b.sig_out = c->d_sig;
+            b.done_ctr = c->d_sig + 2;
+            b.sig_val = ++c->sig_seq;
+        }
+        if (edge_wait) {  // interior(t-K)'s edge sweeps (instead of ev_pre)
+            b.wait_sig = c->d_sig + 3;
+            b.wait_val = edge_prev;
+            b.sig_err = c->d_sig + 1;
+        }
+        // the sweep also writes the next deep halo into the send buffers (no pack kernel)
         HIP_TRY(c, launch_sweepk<T>(b, K, true, bs));
-        HIP_TRY(c, launch_pack_deep_halo<T>(gptr<T>(c, 1 - c->cur), c->L, K, (T*)c->send_left, (T*)c->send_right, bs));
         return IBLB_OK;
     };
     if (ov && c->deep_order == 1) {
         // interior first: the launch the cycle time depends on leaves the host before the RCCL
         // group and the boundary launches; the boundary waits for ev_pre = the compute work
         // before this interior (interior(t-K), which read the columns it overwrites)
-        HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
+        // (signal path: device-side waits, and the compute stream carries the interior launches
+        // alone: no event records or waits between them)
+        if (!edge_wait) HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
         if ((rc = interior())) return rc;
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        if (sig_path) c->int_stale = true;
+        else HIP_TRY(c, rec_int(c));
         if ((rc = exchange_rccl(c, bs, false, false, deep_slots(K)))) return rc;
-        HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_pre, 0));
+        if (!edge_wait) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_pre, 0));
         if ((rc = boundary())) return rc;
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
+        HIP_TRY(c, rec_bnd(c, bs));
+        c->sig_last = sig_path;
+        c->edge_last = sig_path && ni > 0;
     } else {
         if (!ov) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
         if ((rc = exchange_rccl(c, bs, false, false, deep_slots(K)))) return rc;
-        if (ov) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
+        if (ov) HIP_TRY(c, wait_int(c, bs));
         if ((rc = boundary())) return rc;
-        if (ov) HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
+        if (ov) HIP_TRY(c, rec_bnd(c, bs));
         if ((rc = interior())) return rc;
-        if (ov) HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        if (ov) HIP_TRY(c, rec_int(c));
         else {
-            HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-            HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+            HIP_TRY(c, rec_bnd(c, c->stream));
+            HIP_TRY(c, rec_int(c));
             HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
         }
     }
@@ -768,8 +834,8 @@ int band_step(iblb_ctx* c) {
         if ((rc = join_comm(c))) return rc;  // boundary(t-K) wrote columns the interior reads
         if (c->send_deep != K) {            // the send buffers hold another halo: pack the deep one
             HIP_TRY(c, launch_pack_deep_halo<T>(A, c->L, K, (T*)c->send_left, (T*)c->send_right, c->stream));
-            HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-            HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+            HIP_TRY(c, rec_bnd(c, c->stream));
+            HIP_TRY(c, rec_int(c));
             HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
         }
         HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
@@ -803,10 +869,7 @@ int band_step(iblb_ctx* c) {
         d.vs = c->deep_vs;
         d.variant = c->deep_variant;
         if (d.map == 0) d.map = 2;
-        const int per_xcd = std::max(1, c->ncu / 8);
-        if (ov && c->band_reserve % per_xcd == 0) d.xcds = 8 - c->band_reserve / per_xcd;
-        if (slab && c->reserved_cus % per_xcd == 0 && env_long("IBLB_DEEP_XCD_DEAL", 1))
-            d.xcds = 8 - c->reserved_cus / per_xcd;  // the compute stream leaves whole XCDs to the comm stream
+        d.xcds = (int)env_long("IBLB_DEEP_XCDS", 0);  // eight: masks take CUs of every XCD (interior above)
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, ds))) return rc;
         HIP_TRY(c, launch_sweepk<T>(d, K, false, ds));
@@ -864,7 +927,7 @@ int band_step(iblb_ctx* c) {
     if (slab) {
         // comm: deep halo exchange(t) -> (after the compute work before this cycle, which read
         // the columns the boundary sweeps overwrite) boundary sweeps -> deep halo of g^{t+K}
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, rec_int(c));
         hipStream_t cs = c->comm_stream;
         if ((rc = exchange_rccl(c, cs, false, false, deep_slots(K)))) return rc;
         HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_pre, 0));
@@ -872,9 +935,8 @@ int band_step(iblb_ctx* c) {
         b.vs = c->deep_bnd_vs;
         b.variant = c->deep_variant;
         if (b.map == 0) b.map = 2;
-        HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));
-        HIP_TRY(c, launch_pack_deep_halo<T>(B, c->L, K, (T*)c->send_left, (T*)c->send_right, cs));
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));
+        HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));  // also packs the deep halo of B
+        HIP_TRY(c, rec_bnd(c, cs));
         c->send_sweep = false;
         c->send_deep = K;
     }
@@ -901,8 +963,8 @@ int sweep_step(iblb_ctx* c) {
     if (!c->send_sweep) {  // the send buffers hold the one-step (or IB) halo: pack the 2-step one
         HIP_TRY(c, launch_pack_sweep_halo<T>(gptr<T>(c, c->cur), c->L, (T*)c->send_left, (T*)c->send_right,
                                              c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, rec_bnd(c, c->stream));
+        HIP_TRY(c, rec_int(c));
         HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     const bool ov = c->overlap;
@@ -917,11 +979,11 @@ int sweep_step(iblb_ctx* c) {
         if (ni > 0 && (rc = sweep_launch<T>(c, sweep_args<T>(c, 2, W, c->ncol - 2, (ni + W - 1) / W, W), false,
                                             c->stream, true, (long long)ni * c->ny)))
             return rc;
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, rec_int(c));
         if ((rc = exchange_rccl(c, bs, false, true))) return rc;
         HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_pre, 0));
         if ((rc = sweep_launch<T>(c, sweep_args<T>(c, 0, c->ncol - 2, c->ncol, 2, 2), true, bs, false, 0))) return rc;
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
+        HIP_TRY(c, rec_bnd(c, bs));
         after_sweep(c);
         c->send_sweep = true;
         c->send_deep = 0;
@@ -929,17 +991,17 @@ int sweep_step(iblb_ctx* c) {
     }
     if (!ov) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
     if ((rc = exchange_rccl(c, bs, false, true))) return rc;
-    if (ov) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
+    if (ov) HIP_TRY(c, wait_int(c, bs));
     // boundary sweeps: [0, 2) and [ncol-2, ncol)
     if ((rc = sweep_launch<T>(c, sweep_args<T>(c, 0, c->ncol - 2, c->ncol, 2, 2), true, bs, false, 0))) return rc;
-    if (ov) HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
+    if (ov) HIP_TRY(c, rec_bnd(c, bs));
     if (ni > 0 && (rc = sweep_launch<T>(c, sweep_args<T>(c, 2, W, c->ncol - 2, (ni + W - 1) / W, W), false, c->stream,
                                         true, (long long)ni * c->ny)))
         return rc;
-    if (ov) HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+    if (ov) HIP_TRY(c, rec_int(c));
     else {
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, rec_bnd(c, c->stream));
+        HIP_TRY(c, rec_int(c));
         HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     after_sweep(c);
@@ -961,8 +1023,8 @@ int advance(iblb_ctx* c) {
         if (rc) return rc;
     }
     if (rccl_multi(c)) {  // the whole state was written on the compute stream
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, rec_bnd(c, c->stream));
+        HIP_TRY(c, rec_int(c));
         HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     after_step(c);
@@ -1275,6 +1337,7 @@ void iblb_destroy(iblb_ctx* c) {
         if (c->band_pin[i]) (void)hipHostFree(c->band_pin[i]);
     }
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
+    if (c->d_sig) (void)hipFree(c->d_sig);
     if (c->ev_int) (void)hipEventDestroy(c->ev_int);
     if (c->ev_pre) (void)hipEventDestroy(c->ev_pre);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -1358,8 +1421,9 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
 }  // extern "C"
 
 // Streams of the overlapped band cycle (lone slab): the band chain on band_st restricted to
-// `band_reserve` CUs (whole XCDs at the top, like the RCCL comm stream's), the cycle's deep sweep
-// on deep_st masked to the other CUs.  The context's stream is never replaced: it keeps the
+// `band_reserve` CUs (the top mask bits, like the RCCL comm stream's: bit i is a CU of XCD i % 8,
+// so 32 bits are four CUs of every XCD, profiles/r02n_xcc_probe.txt), the cycle's deep sweep on
+// deep_st masked to the other CUs.  The context's stream is never replaced: it keeps the
 // whole chip for every other launch and joins the two with events in band_step.  Default: one
 // XCD, two where the band trapezoids hold more than 5 % of the cycle's lattice updates (one-step
 // launches, HBM-bound; the deep sweep is issue-bound).  IBLB_BAND_RESERVE_CUS=0: both on the
@@ -1930,6 +1994,11 @@ int iblb_synchronize(iblb_ctx* c) {
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));
+    if (c->d_sig) {
+        unsigned err = 0;
+        HIP_TRY(c, hipMemcpy(&err, c->d_sig + 1, sizeof(err), hipMemcpyDeviceToHost));
+        if (err) return fail(c, IBLB_ERR_COMM, "deep slab interior gave up waiting for the boundary signal");
+    }
     return IBLB_OK;
 }
 
@@ -2099,10 +2168,11 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
             const int wpc = c->prec == IBLB_PREC_F64
                                 ? sweepk_geometry<double>(c->sweep_depth, c->deep_bnd_vs, c->deep_variant, true, c->ny, &nch)
                                 : sweepk_geometry<float>(c->sweep_depth, c->deep_bnd_vs, c->deep_variant, true, c->ny, &nch);
-            // whole XCDs (ncu / 8 CUs each): a partly reserved XCD is the straggler of every
-            // interior launch (self ring, deep slab 512 / 1024 / 2048 x 4096: 0.0376 / 0.0564 /
-            // 0.0953 ms/iteration with 32 CUs, 0.046 / 0.080 / 0.148 with 16, 0.049 / 0.087 /
-            // 0.164 with 40; profiles/r01e5_gap_probe_reserve.txt)
+            // rounded up to multiples of ncu / 8 (the top mask bits take the same number of CUs
+            // from every XCD, profiles/r02n_xcc_probe.txt); 32 measured best (self ring, deep
+            // slab 512 / 1024 / 2048 x 4096: 0.0376 / 0.0564 / 0.0953 ms/iteration with 32 CUs,
+            // 0.046 / 0.080 / 0.148 with 16, 0.049 / 0.087 / 0.164 with 40;
+            // profiles/r01e5_gap_probe_reserve.txt)
             if (wpc > 0) {
                 const long need = std::max(8L, (long)((2 * nch + wpc - 1) / wpc));
                 const long xcd = std::max(1, c->ncu / 8);
@@ -2112,10 +2182,12 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         if (reserve > 0) {
             const int ncu = c->ncu;
             if (reserve >= ncu) return fail(c, IBLB_ERR_ARG, "IBLB_RESERVE_CUS exceeds the compute units");
-            // Which CUs: the top ones (the last XCD first).  The dispatcher deals workgroups
-            // round-robin over the XCDs, so for long launches only whole XCDs should be reserved
-            // (above); IBLB_RESERVE_LAYOUT=1 takes the same number from every XCD instead
-            // (measured slower: 0.0486 vs 0.0376 ms/iteration with 32, profiles/r01e4_*).
+            // Which CUs: the top mask bits.  Bit i is a CU of XCD i % 8 and the dispatcher deals
+            // workgroups round-robin over all eight XCDs whatever the mask (an XCD left without
+            // any bit runs on all its CUs), so the top 32 bits are four CUs of every XCD
+            // (profiles/r02n_xcc_probe.txt).  IBLB_RESERVE_LAYOUT=1 picks bits 31, 63, ..., i.e.
+            // all of XCD 7, which then falls back to unmasked: measured slower (0.0486 vs
+            // 0.0376 ms/iteration with 32, profiles/r01e4_*).
             const bool xcd_major = env_long("IBLB_RESERVE_LAYOUT", 0) == 1 && ncu % 8 == 0;
             if (xcd_major) reserve = (reserve + 7) / 8 * 8;
             if (reserve >= ncu) return fail(c, IBLB_ERR_ARG, "IBLB_RESERVE_CUS exceeds the compute units");
@@ -2149,8 +2221,15 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_pre, evf));
         c->sweep_order = (int)env_long("IBLB_SWEEP_ORDER", 0);
         c->deep_order = (int)env_long("IBLB_DEEP_ORDER", 1);
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        // device-side boundary signal (not with the in-process RCCL stand-in of the tests: its
+        // ranks share one GPU and their spinning interiors could hold the CUs another rank needs)
+        c->slab_signal = env_long("IBLB_SLAB_SIGNAL", 0) != 0 && !(&iblb_mock_rccl && iblb_mock_rccl());
+        if (!c->d_sig) HIP_TRY(c, hipMalloc(&c->d_sig, 8 * sizeof(unsigned)));
+        HIP_TRY(c, hipMemsetAsync(c->d_sig, 0, 8 * sizeof(unsigned), c->stream));
+        c->sig_seq = c->edge_seq = 0;
+        c->sig_last = c->edge_last = false;
+        HIP_TRY(c, rec_bnd(c, c->stream));  // send buffers of the current state
+        HIP_TRY(c, rec_int(c));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
     }
     c->halo_valid = false;

@@ -82,6 +82,13 @@ struct Sweep2Args {
     int xcds;            // deep sweeps, map 2: XCDs the workgroups are dealt over (0 = 8)
     const int* sweep_tab;  // deep sweeps: sweep s covers [sweep_tab[2s], sweep_tab[2s+1]) (device;
                            // nullptr: col_begin / col_step / W); the force-free gaps between IB bands
+    const unsigned* wait_sig;  // deep slab interior: every wave first waits until *wait_sig reaches
+    unsigned wait_val;         //   wait_val (released by the previous cycle's boundary sweeps);
+    unsigned* sig_err;         //   bounded, *sig_err = 1 on timeout
+    unsigned* sig_out;         // the last wave to finish (counted in *done_ctr, reset by it) releases
+    unsigned* done_ctr;        //   *sig_out = sig_val: every wave of a deep slab boundary launch, or
+    unsigned sig_val;          //   (edge_w > 0) the waves of the first and last sweep of an interior
+    int edge_w;                // interior, balanced: first and last sweep edge_w (>= K) columns wide
     int flux_col;        // local column sampled for Q (both iterations), or -1
     double flux_norm;
     double* Q;
@@ -95,7 +102,9 @@ template <typename T>
 hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s);
 // K = depth (3 .. 6) iterations per launch: g^t -> g^{t+K}; map 1 or 2.  slab = false: lone
 // slab (periodic columns) or interior columns of a group slab; slab = true: columns beyond the
-// edges from the deep halo (deep_slot) in recv_left / recv_right.  col_step 0: balanced widths.
+// edges from the deep halo (deep_slot) in recv_left / recv_right, and (send_left != nullptr) the
+// output columns [0, K) / [ncol-K, ncol) also written into the deep halo of the send buffers
+// (what launch_pack_deep_halo makes of them).  col_step 0: balanced widths.
 template <typename T>
 hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool slab, hipStream_t s);
 // Resident waves per CU of a deep-sweep configuration; *nch = its row chunks for ny rows.
