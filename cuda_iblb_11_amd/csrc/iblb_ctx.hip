@@ -24,8 +24,6 @@
 
 #include "../../include/iblb.h"
 
-// defined only by the tests' in-process RCCL stand-in (tests/mock_rccl/mock_rccl.cpp)
-extern "C" __attribute__((weak)) int iblb_mock_rccl(void);
 #include "cilia_kernels.h"
 #include "iblb_kernels.h"
 
@@ -69,6 +67,7 @@ struct iblb_ctx {
     // K = 3 .. 6 iterations per launch on a lone slab (IBLB_SWEEP_DEPTH): columns per wave, cells per lane
     int sweep_depth = 2, deep_w = 4, deep_vs = 2, deep_variant = 1, deep_balance = 1, deep_bnd_vs = 2, deep_slab_vs = 1;
     int reserved_cus = 0, ncu = 0;  // CUs kept free of the compute stream (RCCL groups), device CUs
+    std::vector<uint32_t> comp_mask;  // the compute stream's CU mask when reserved_cus > 0
     hipStream_t stream = nullptr;
     Coef coef{};
     KConst kc{};  // collide constants folded from coef (kernel arguments)
@@ -163,14 +162,9 @@ struct iblb_ctx {
     hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with the interior
     hipEvent_t ev_bnd = nullptr;  // boundary columns + send buffers of the state written (either stream)
     hipEvent_t ev_int = nullptr;  // compute-stream work of the last step done
-    unsigned* d_sig = nullptr;    // deep slab cycle: [0] boundary signal, [1] wait timeout flag,
-                                  // [2] boundary waves done (counter of the running launch)
-    unsigned sig_seq = 0;         // value the last boundary sweep released
-    unsigned edge_seq = 0;        // value the last interior's edge sweeps release ([3], counter [4])
-    bool edge_last = false;       // ... and that interior was the last compute work of a deep cycle
-    bool int_stale = false;       // ev_int not recorded after the last deep cycle's interior
-    bool sig_last = false;        // ev_bnd's last record followed that signal (nothing else since)
-    bool slab_signal = false;     // IBLB_SLAB_SIGNAL: interiors wait on d_sig instead of ev_bnd
+    bool deep_chain = false;      // the last compute work is a deep slab cycle's (interior first) ...
+    long long deep_chain_t = -1;  // ... that ended at this t with this cur: ev_int follows its interior
+    int deep_chain_cur = -1;
     hipEvent_t ev_pre = nullptr;  // compute-stream work before the interior sweep (sweep order 1)
     bool overlap = true;
     int sweep_order = 0;          // IBLB_SWEEP_ORDER: 1 = the host submits the interior sweep first
@@ -334,29 +328,6 @@ int ev_end(iblb_ctx* c, size_t idx, int kind, long long cells = 0, hipStream_t s
 }
 
 // ---- halo exchange ----------------------------------------------------------------------
-// ev_bnd marks "boundary columns and send buffers of the current state written"; a record by
-// anything but the deep slab cycle's signal path ends that path's device-side signal chain.
-static hipError_t rec_bnd(iblb_ctx* c, hipStream_t st) {
-    c->sig_last = false;
-    return hipEventRecord(c->ev_bnd, st);
-}
-static hipError_t rec_int(iblb_ctx* c) {
-    c->int_stale = false;
-    c->edge_last = false;
-    return hipEventRecord(c->ev_int, c->stream);
-}
-// st after the compute work of the last step (ev_int; the deep cycle's signal path leaves it to be
-// recorded here, on demand: a later record on the compute stream covers the same work and more)
-static hipError_t wait_int(iblb_ctx* c, hipStream_t st) {
-    c->edge_last = false;  // another step follows
-    if (c->int_stale) {
-        hipError_t e = hipEventRecord(c->ev_int, c->stream);
-        if (e != hipSuccess) return e;
-        c->int_stale = false;
-    }
-    return hipStreamWaitEvent(st, c->ev_int, 0);
-}
-
 // IB slots of the send buffers (slots 0-2 come from the collide)
 template <typename T>
 int pack_ib(iblb_ctx* c, hipStream_t st) {
@@ -419,8 +390,8 @@ int pack_send(iblb_ctx* c) {
     c->send_sweep = false;
     c->send_deep = 0;
     if (rccl_multi(c)) {
-        HIP_TRY(c, rec_bnd(c, c->stream));
-        HIP_TRY(c, rec_int(c));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     return IBLB_OK;
@@ -549,11 +520,11 @@ template <typename T>
 int overlapped_step(iblb_ctx* c) {
     int rc = exchange_rccl(c, c->comm_stream);
     if (rc) return rc;
-    HIP_TRY(c, wait_int(c, c->comm_stream));
+    HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_int, 0));
     if ((rc = launch_fused_step<T>(c, 0, 2, c->ncol - 1, false, c->comm_stream))) return rc;
-    HIP_TRY(c, rec_bnd(c, c->comm_stream));
+    HIP_TRY(c, hipEventRecord(c->ev_bnd, c->comm_stream));
     if ((rc = launch_fused_step<T>(c, 1, c->ncol - 2))) return rc;
-    HIP_TRY(c, rec_int(c));
+    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
     after_step(c);
     return IBLB_OK;
 }
@@ -578,7 +549,7 @@ int ib_overlapped_step(iblb_ctx* c, int next) {
     HIP_TRY(c, launch_ib_slab<T>(gptr<T>(c, c->cur), c->L, X, c->nx, c->x_begin, c->ns, pts_s(c), pts_us(c), pts_eps(c),
                                  c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, c->stream, 1));
     HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
-    HIP_TRY(c, wait_int(c, bs));
+    HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
     if ((rc = exchange_rccl(c, bs, true))) return rc;
     HIP_TRY(c, launch_ib_slab<T>(gptr<T>(c, c->cur), c->L, X, c->nx, c->x_begin, c->ns, pts_s(c), pts_us(c), pts_eps(c),
                                  c->d_Fs, c->fdense, c->fplane, c->flags, c->nch, 64 * c->V, bs, 2));
@@ -587,9 +558,9 @@ int ib_overlapped_step(iblb_ctx* c, int next) {
     HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_pre, 0));
     if ((rc = launch_fused_step<T>(c, 0, 3, 1, false, bs))) return rc;
     if ((rc = launch_fused_step<T>(c, c->ncol - 3, 3, 1, false, bs))) return rc;
-    HIP_TRY(c, rec_bnd(c, bs));
+    HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
     if ((rc = launch_fused_step<T>(c, 3, c->ncol - 6))) return rc;
-    HIP_TRY(c, rec_int(c));
+    HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
     after_step(c);
     return IBLB_OK;
 }
@@ -661,27 +632,20 @@ void after_sweep(iblb_ctx* c) {
 // (deep_slots(K) column-planes per side) exchanged and the boundary sweeps (output columns
 // [0, K) and [ncol-K, ncol), which then pack the deep halo of the new state) on the comm stream
 // beside the interior sweep [K, ncol-K), as sweep_step does for two iterations:
-//   comm:    exchange(t) -> wait int(t-K) -> boundary(t) -> pack halo(t+K) -> ev_bnd
+//   comm:    exchange(t) -> wait int(t-K) -> boundary(t) [+ deep halo of g^{t+K}] -> ev_bnd
 //   compute: (join_comm: boundary(t-K)) -> interior(t) -> ev_int
 template <typename T>
 int deep_slab_step(iblb_ctx* c) {
     const int K = c->sweep_depth;
     const int W = std::max(1, c->deep_w);
     const bool ov = c->overlap;
-    // signal path: the previous cycle's boundary released d_sig; the interior waits for it on the
-    // device (slab_wait) and the compute stream carries no cross-stream wait
-    const bool sig_path = ov && c->deep_order == 1 && c->slab_signal;
-    const bool sig_wait = sig_path && c->sig_last && c->send_deep == K;
-    // ... and the boundary waits for the previous interior's edge sweeps, not for all of it
-    const bool edge_wait = sig_wait && c->edge_last;
-    const unsigned edge_prev = c->edge_seq;
-    int rc = sig_wait ? IBLB_OK : join_comm(c);
+    int rc = join_comm(c);
     if (rc) return rc;
     if (c->send_deep != K) {  // the send buffers hold another halo: pack the deep one now
         HIP_TRY(c, launch_pack_deep_halo<T>(gptr<T>(c, c->cur), c->L, K, (T*)c->send_left, (T*)c->send_right,
                                             c->stream));
-        HIP_TRY(c, rec_bnd(c, c->stream));
-        HIP_TRY(c, rec_int(c));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     hipStream_t bs = ov ? c->comm_stream : c->stream;
@@ -696,17 +660,6 @@ int deep_slab_step(iblb_ctx* c) {
         a.xcds = (int)env_long("IBLB_DEEP_XCDS", 0);
         a.variant = c->deep_variant;
         if (a.map == 0) a.map = 2;
-        if (sig_wait) {
-            a.wait_sig = c->d_sig;
-            a.wait_val = c->sig_seq;
-            a.sig_err = c->d_sig + 1;
-        }
-        if (sig_path) {  // its first and last sweeps (edge_w columns) release the edge signal
-            a.edge_w = std::max(K, (int)env_long("IBLB_DEEP_EDGE_W", K));
-            a.sig_out = c->d_sig + 3;
-            a.done_ctr = c->d_sig + 4;
-            a.sig_val = ++c->edge_seq;
-        }
         size_t ev = 0;
         int r = ev_begin(c, &ev, c->stream);
         if (r) return r;
@@ -718,47 +671,41 @@ int deep_slab_step(iblb_ctx* c) {
         b.vs = c->deep_bnd_vs;
         b.variant = c->deep_variant;
         if (b.map == 0) b.map = 2;
-        if (sig_path) {  // its last wave releases the signal the next interior waits for
-            b.sig_out = c->d_sig;
-            b.done_ctr = c->d_sig + 2;
-            b.sig_val = ++c->sig_seq;
-        }
-        if (edge_wait) {  // interior(t-K)'s edge sweeps (instead of ev_pre)
-            b.wait_sig = c->d_sig + 3;
-            b.wait_val = edge_prev;
-            b.sig_err = c->d_sig + 1;
-        }
         // the sweep also writes the next deep halo into the send buffers (no pack kernel)
         HIP_TRY(c, launch_sweepk<T>(b, K, true, bs));
         return IBLB_OK;
     };
+    bool chain = false;
     if (ov && c->deep_order == 1) {
         // interior first: the launch the cycle time depends on leaves the host before the RCCL
-        // group and the boundary launches; the boundary waits for ev_pre = the compute work
-        // before this interior (interior(t-K), which read the columns it overwrites)
-        // (signal path: device-side waits, and the compute stream carries the interior launches
-        // alone: no event records or waits between them)
-        if (!edge_wait) HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
+        // group and the boundary launches.  The boundary waits for ev_int = the compute work
+        // before this interior (interior(t-K), which read the columns it overwrites and wrote the
+        // ones it reads).  Cycles back to back: the previous cycle recorded ev_int right after
+        // interior(t-K), and ev_int is recorded again only after this cycle's boundary has taken
+        // its wait, so the compute stream carries one wait and one record per cycle (each
+        // cross-queue packet idles the compute queue for microseconds: 512 x 4096 self ring,
+        // profiles/r02q_*: ~14 us per cycle between two interior sweeps with four of them, ~3 us
+        // between back-to-back sweeps of a lone slab).
+        if (!(c->deep_chain && c->deep_chain_t == c->t && c->deep_chain_cur == c->cur))
+            HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         if ((rc = interior())) return rc;
-        if (sig_path) c->int_stale = true;
-        else HIP_TRY(c, rec_int(c));
         if ((rc = exchange_rccl(c, bs, false, false, deep_slots(K)))) return rc;
-        if (!edge_wait) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_pre, 0));
+        HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
         if ((rc = boundary())) return rc;
-        HIP_TRY(c, rec_bnd(c, bs));
-        c->sig_last = sig_path;
-        c->edge_last = sig_path && ni > 0;
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        chain = true;
     } else {
         if (!ov) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
         if ((rc = exchange_rccl(c, bs, false, false, deep_slots(K)))) return rc;
-        if (ov) HIP_TRY(c, wait_int(c, bs));
+        if (ov) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
         if ((rc = boundary())) return rc;
-        if (ov) HIP_TRY(c, rec_bnd(c, bs));
+        if (ov) HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
         if ((rc = interior())) return rc;
-        if (ov) HIP_TRY(c, rec_int(c));
+        if (ov) HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         else {
-            HIP_TRY(c, rec_bnd(c, c->stream));
-            HIP_TRY(c, rec_int(c));
+            HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+            HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
             HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
         }
     }
@@ -767,6 +714,9 @@ int deep_slab_step(iblb_ctx* c) {
     c->halo_valid = false;
     c->send_sweep = false;
     c->send_deep = K;
+    c->deep_chain = chain;
+    c->deep_chain_t = c->t;
+    c->deep_chain_cur = c->cur;
     return IBLB_OK;
 }
 
@@ -834,8 +784,8 @@ int band_step(iblb_ctx* c) {
         if ((rc = join_comm(c))) return rc;  // boundary(t-K) wrote columns the interior reads
         if (c->send_deep != K) {            // the send buffers hold another halo: pack the deep one
             HIP_TRY(c, launch_pack_deep_halo<T>(A, c->L, K, (T*)c->send_left, (T*)c->send_right, c->stream));
-            HIP_TRY(c, rec_bnd(c, c->stream));
-            HIP_TRY(c, rec_int(c));
+            HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+            HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
             HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
         }
         HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
@@ -927,7 +877,7 @@ int band_step(iblb_ctx* c) {
     if (slab) {
         // comm: deep halo exchange(t) -> (after the compute work before this cycle, which read
         // the columns the boundary sweeps overwrite) boundary sweeps -> deep halo of g^{t+K}
-        HIP_TRY(c, rec_int(c));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         hipStream_t cs = c->comm_stream;
         if ((rc = exchange_rccl(c, cs, false, false, deep_slots(K)))) return rc;
         HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_pre, 0));
@@ -936,7 +886,7 @@ int band_step(iblb_ctx* c) {
         b.variant = c->deep_variant;
         if (b.map == 0) b.map = 2;
         HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));  // also packs the deep halo of B
-        HIP_TRY(c, rec_bnd(c, cs));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));
         c->send_sweep = false;
         c->send_deep = K;
     }
@@ -963,8 +913,8 @@ int sweep_step(iblb_ctx* c) {
     if (!c->send_sweep) {  // the send buffers hold the one-step (or IB) halo: pack the 2-step one
         HIP_TRY(c, launch_pack_sweep_halo<T>(gptr<T>(c, c->cur), c->L, (T*)c->send_left, (T*)c->send_right,
                                              c->stream));
-        HIP_TRY(c, rec_bnd(c, c->stream));
-        HIP_TRY(c, rec_int(c));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     const bool ov = c->overlap;
@@ -979,11 +929,11 @@ int sweep_step(iblb_ctx* c) {
         if (ni > 0 && (rc = sweep_launch<T>(c, sweep_args<T>(c, 2, W, c->ncol - 2, (ni + W - 1) / W, W), false,
                                             c->stream, true, (long long)ni * c->ny)))
             return rc;
-        HIP_TRY(c, rec_int(c));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         if ((rc = exchange_rccl(c, bs, false, true))) return rc;
         HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_pre, 0));
         if ((rc = sweep_launch<T>(c, sweep_args<T>(c, 0, c->ncol - 2, c->ncol, 2, 2), true, bs, false, 0))) return rc;
-        HIP_TRY(c, rec_bnd(c, bs));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
         after_sweep(c);
         c->send_sweep = true;
         c->send_deep = 0;
@@ -991,17 +941,17 @@ int sweep_step(iblb_ctx* c) {
     }
     if (!ov) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
     if ((rc = exchange_rccl(c, bs, false, true))) return rc;
-    if (ov) HIP_TRY(c, wait_int(c, bs));
+    if (ov) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
     // boundary sweeps: [0, 2) and [ncol-2, ncol)
     if ((rc = sweep_launch<T>(c, sweep_args<T>(c, 0, c->ncol - 2, c->ncol, 2, 2), true, bs, false, 0))) return rc;
-    if (ov) HIP_TRY(c, rec_bnd(c, bs));
+    if (ov) HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
     if (ni > 0 && (rc = sweep_launch<T>(c, sweep_args<T>(c, 2, W, c->ncol - 2, (ni + W - 1) / W, W), false, c->stream,
                                         true, (long long)ni * c->ny)))
         return rc;
-    if (ov) HIP_TRY(c, rec_int(c));
+    if (ov) HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
     else {
-        HIP_TRY(c, rec_bnd(c, c->stream));
-        HIP_TRY(c, rec_int(c));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     after_sweep(c);
@@ -1023,8 +973,8 @@ int advance(iblb_ctx* c) {
         if (rc) return rc;
     }
     if (rccl_multi(c)) {  // the whole state was written on the compute stream
-        HIP_TRY(c, rec_bnd(c, c->stream));
-        HIP_TRY(c, rec_int(c));
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
     }
     after_step(c);
@@ -1337,7 +1287,6 @@ void iblb_destroy(iblb_ctx* c) {
         if (c->band_pin[i]) (void)hipHostFree(c->band_pin[i]);
     }
     if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
-    if (c->d_sig) (void)hipFree(c->d_sig);
     if (c->ev_int) (void)hipEventDestroy(c->ev_int);
     if (c->ev_pre) (void)hipEventDestroy(c->ev_pre);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -1355,6 +1304,7 @@ void iblb_destroy(iblb_ctx* c) {
 
 int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double* f, const double* force) {
     if (!c) return IBLB_ERR_ARG;
+    c->deep_chain = false;  // the state is rewritten: no deep cycle chain across this
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     const long N = (long)c->ncol * c->ny;
@@ -1994,11 +1944,6 @@ int iblb_synchronize(iblb_ctx* c) {
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->comm_stream) HIP_TRY(c, hipStreamSynchronize(c->comm_stream));
-    if (c->d_sig) {
-        unsigned err = 0;
-        HIP_TRY(c, hipMemcpy(&err, c->d_sig + 1, sizeof(err), hipMemcpyDeviceToHost));
-        if (err) return fail(c, IBLB_ERR_COMM, "deep slab interior gave up waiting for the boundary signal");
-    }
     return IBLB_OK;
 }
 
@@ -2110,6 +2055,7 @@ int iblb_rccl_unique_id(char id[IBLB_UNIQUE_ID_BYTES]) {
 
 int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nranks, int rank) {
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return IBLB_ERR_ARG;
+    c->deep_chain = false;  // the state is rewritten: no deep cycle chain across this
     if (c->transport != TR_NONE) return fail(c, IBLB_ERR_STATE, "context already linked");
     HIP_TRY(c, hipSetDevice(c->device));
     ncclUniqueId u;
@@ -2201,6 +2147,7 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
             hipStream_t masked = nullptr;
             HIP_TRY(c, hipExtStreamCreateWithCUMask(&masked, (uint32_t)mask.size(), mask.data()));
             c->reserved_cus = (int)reserve;
+            c->comp_mask = mask;
             HIP_TRY(c, hipStreamSynchronize(c->stream));
             (void)hipStreamDestroy(c->stream);
             c->stream = masked;
@@ -2208,7 +2155,16 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         int prio_lo = 0, prio_hi = 0;
         HIP_TRY(c, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
         const int prio = env_long("IBLB_COMM_PRIORITY", 1) != 0 ? prio_hi : prio_lo;
-        HIP_TRY(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
+        if (c->reserved_cus > 0 && env_long("IBLB_COMM_MASK", 1) != 0) {
+            // the comm stream confined to the reserved CUs: a boundary sweep dispatched before the
+            // interior of the same cycle must not take CUs the interior's round of waves needs
+            std::vector<uint32_t> m(c->comp_mask.size(), 0u);
+            for (int i = 0; i < c->ncu; ++i)
+                if (!(c->comp_mask[(size_t)i / 32] >> (i % 32) & 1u)) m[(size_t)i / 32] |= 1u << (i % 32);
+            HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->comm_stream, (uint32_t)m.size(), m.data()));
+        } else {
+            HIP_TRY(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
+        }
         // cross-stream ordering events (producer and consumer on this device): IBLB_EVENT_FENCE
         // 0 = HIP's default system-scope release / acquire, 1 = hipEventDisableSystemFence
         // (default: 512 x 4096 self ring 0.0394 vs 0.0420 ms/iteration, 1024 0.0682 vs 0.0705,
@@ -2221,15 +2177,9 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_pre, evf));
         c->sweep_order = (int)env_long("IBLB_SWEEP_ORDER", 0);
         c->deep_order = (int)env_long("IBLB_DEEP_ORDER", 1);
-        // device-side boundary signal (not with the in-process RCCL stand-in of the tests: its
-        // ranks share one GPU and their spinning interiors could hold the CUs another rank needs)
-        c->slab_signal = env_long("IBLB_SLAB_SIGNAL", 0) != 0 && !(&iblb_mock_rccl && iblb_mock_rccl());
-        if (!c->d_sig) HIP_TRY(c, hipMalloc(&c->d_sig, 8 * sizeof(unsigned)));
-        HIP_TRY(c, hipMemsetAsync(c->d_sig, 0, 8 * sizeof(unsigned), c->stream));
-        c->sig_seq = c->edge_seq = 0;
-        c->sig_last = c->edge_last = false;
-        HIP_TRY(c, rec_bnd(c, c->stream));  // send buffers of the current state
-        HIP_TRY(c, rec_int(c));
+
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));  // send buffers of the current state
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
     }
     c->halo_valid = false;
@@ -2377,6 +2327,7 @@ int iblb_save_checkpoint(iblb_ctx* c, const char* path) {
 
 int iblb_load_checkpoint(iblb_ctx* c, const char* path) {
     if (!c || !path) return IBLB_ERR_ARG;
+    c->deep_chain = false;  // the state is rewritten: no deep cycle chain across this
     if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: restore the slabs before linking");
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));

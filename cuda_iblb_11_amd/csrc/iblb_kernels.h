@@ -82,13 +82,6 @@ struct Sweep2Args {
     int xcds;            // deep sweeps, map 2: XCDs the workgroups are dealt over (0 = 8)
     const int* sweep_tab;  // deep sweeps: sweep s covers [sweep_tab[2s], sweep_tab[2s+1]) (device;
                            // nullptr: col_begin / col_step / W); the force-free gaps between IB bands
-    const unsigned* wait_sig;  // deep slab interior: every wave first waits until *wait_sig reaches
-    unsigned wait_val;         //   wait_val (released by the previous cycle's boundary sweeps);
-    unsigned* sig_err;         //   bounded, *sig_err = 1 on timeout
-    unsigned* sig_out;         // the last wave to finish (counted in *done_ctr, reset by it) releases
-    unsigned* done_ctr;        //   *sig_out = sig_val: every wave of a deep slab boundary launch, or
-    unsigned sig_val;          //   (edge_w > 0) the waves of the first and last sweep of an interior
-    int edge_w;                // interior, balanced: first and last sweep edge_w (>= K) columns wide
     int flux_col;        // local column sampled for Q (both iterations), or -1
     double flux_norm;
     double* Q;

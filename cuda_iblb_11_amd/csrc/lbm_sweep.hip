@@ -538,7 +538,8 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
 #pragma unroll
             for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * a.L.plane, off, out[k]);
             // slab of a group: the output columns within K of an edge are the deep halo the
-            // neighbour needs next cycle (wave-uniform: c is the walk's column)
+            // neighbour needs next cycle (wave-uniform: c is the walk's column); written here
+            // instead of by a pack kernel after the sweep
             if (SLAB && a.send_left && (c < K || c >= a.L.ncol - K)) {
                 const bool to_left = c < K;
                 const int d = to_left ? c : a.L.ncol - 1 - c;
@@ -580,8 +581,8 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
 }
 
 // wave -> (sweep, chunk) of the linear order, optionally dealt to the XCDs in contiguous ranges
-// (xcds: the XCDs the launch's workgroups are dealt over; a stream whose CU mask leaves whole
-// XCDs out deals over the others)
+// (xcds: the XCDs the launch's workgroups are dealt over, 0 = 8; the dispatcher deals over all
+// eight whatever the stream's CU mask, profiles/r02n_xcc_probe.txt)
 __device__ __forceinline__ void linear_item(int map, int nch, int xcds, int wv, int& sw, int& ch) {
     int b = (int)blockIdx.x;
     if (map == 2) {
@@ -592,43 +593,6 @@ __device__ __forceinline__ void linear_item(int map, int nch, int xcds, int wv, 
     const int gw = b * 4 + wv;
     sw = gw / nch;
     ch = gw - sw * nch;
-}
-
-// Deep slab interior: wait for the previous cycle's boundary sweeps (they write columns this
-// launch reads, and read columns it overwrites) through the counter launch_slab_signal releases on
-// the comm stream, instead of a cross-stream event wait between the two interior launches (that
-// wait cost ~14 us per 5-iteration cycle at 512 x 4096, profiles/r02q_*).  The boundary runs on
-// CUs the interior's stream mask leaves out, so it progresses while these waves wait.  Bounded:
-// after ~0.5 s the wave gives up and flags *err (the host reports it) rather than hang the device.
-// The poll is a relaxed load (no cache invalidation per poll: an acquire load in the loop made
-// every waiting wave invalidate its caches each time round and slowed the boundary sweeps and
-// RCCL kernels running beside it ~1.7x); one acquire fence after the wait.
-__device__ __noinline__ void slab_wait(const unsigned* sig, unsigned v, unsigned* err, int lane) {
-    for (int n = 0; (int)(__hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - v) < 0; ++n) {
-        if (n > (1 << 20)) {
-            if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(16);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
-// Called once by every counted wave after its stores (deep slab boundary: every wave of the
-// launch, early exits included; interior: the waves of the two edge sweeps).  The wave's stores
-// are released before it is counted; the wave that completes the count resets the counter and
-// releases the signal (no signal kernel, no event between the streams): the boundary's tells the
-// next interior its columns are written, the interior edges' tell the next boundary that the
-// columns it reads are written and the ones it overwrites are read.
-template <typename T>
-__device__ __forceinline__ void slab_wave_done(const Sweep2Args<T>& a, int lane, unsigned total) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if (lane == 0) {
-        if (__hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
-            __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.sig_out, a.sig_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 template <int K, int VS>
@@ -643,11 +607,7 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int sw, ch;
     linear_item(a.map, a.nch, a.xcds, wv, sw, ch);
-    if (sw >= a.nsweep || ch >= a.nch) {
-        if (SLAB && a.sig_out) slab_wave_done(a, lane, gridDim.x * (blockDim.x / 64));
-        return;
-    }
-    if (a.wait_sig) slab_wait(a.wait_sig, a.wait_val, a.sig_err, lane);
+    if (sw >= a.nsweep || ch >= a.nch) return;
     int xa, xb;
     if (a.sweep_tab) {
         xa = __builtin_amdgcn_readfirstlane(a.sweep_tab[2 * sw]);
@@ -655,16 +615,6 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     } else if (a.col_step > 0) {
         xa = a.col_begin + sw * a.col_step;
         xb = min(xa + a.W, a.col_end);
-    } else if (a.edge_w > 0) {  // narrow first / last sweep, the others balanced in between
-        const int ew = a.edge_w;
-        if (sw == 0 || sw == a.nsweep - 1) {
-            xa = sw == 0 ? a.col_begin : a.col_end - ew;
-            xb = xa + ew;
-        } else {
-            const long n = a.col_end - a.col_begin - 2 * ew;
-            xa = a.col_begin + ew + (int)((sw - 1) * n / (a.nsweep - 2));
-            xb = a.col_begin + ew + (int)(sw * n / (a.nsweep - 2));
-        }
     } else {  // balanced: nsweep sweeps of floor/ceil((col_end - col_begin) / nsweep) columns
         const long n = a.col_end - a.col_begin;
         xa = a.col_begin + (int)(sw * n / a.nsweep);
@@ -687,12 +637,6 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     if (a.flux_col >= xa && a.flux_col < xb) {
         const double qs = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, qs);
-    }
-    if (a.sig_out) {
-        if (SLAB)
-            slab_wave_done(a, lane, gridDim.x * (blockDim.x / 64));
-        else if (sw == 0 || sw == a.nsweep - 1)
-            slab_wave_done(a, lane, (unsigned)((a.nsweep > 1 ? 2 : 1) * a.nch));
     }
 }
 
@@ -731,18 +675,6 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s) {
             ns = std::max(1L, rounds * slots / b.nch);
         }
         b.nsweep = (int)std::min(ns, n);
-        // narrow edge sweeps: at least three sweeps, each middle one a column or more; a short
-        // interior is one sweep (its waves all count as edge waves)
-        if (b.edge_w > 0) {
-            if (n <= 2L * b.edge_w) {
-                b.nsweep = 1;
-                b.edge_w = 0;
-            } else {
-                b.nsweep = (int)std::min(std::max(3L, (long)b.nsweep), n - 2L * b.edge_w + 2);
-            }
-        }
-    } else {
-        b.edge_w = 0;
     }
     const unsigned blocks = (unsigned)(((long)b.nsweep * b.nch + 3) / 4);
     sweepk_kernel<T, VS, MODE, K, SLAB><<<blocks, 256, 0, s>>>(b);

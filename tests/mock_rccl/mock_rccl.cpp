@@ -256,6 +256,3 @@ ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcoun
 }
 
 }  // extern "C"
-
-// Marks this build as the stand-in: libiblb keeps its deep slab cycle on event waits here.
-extern "C" int iblb_mock_rccl(void) { return 1; }

@@ -449,17 +449,16 @@ def test_interleaved_layout_identical(gpu, monkeypatch, precision):
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
-@pytest.mark.parametrize("overlap,order,signal", [(1, 0, 1), (0, 0, 1), (1, 1, 1), (1, 1, 0)])
+@pytest.mark.parametrize("overlap,order", [(1, 0), (0, 0), (1, 1)])
 @pytest.mark.parametrize("depth", [2, 5])
-def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap, order, signal, depth):
+def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap, order, depth):
     """Bulk stepping of an RCCL group over real RCCL (self ring), readers interleaved: the
     multi-iteration sweeps (depth 2: 2-step halo; depth 5: the deep halo, 39 column-planes per
     side) with the boundary sweeps on the comm stream beside the interior sweep, shorter sweeps
     and one-step launches for the remainders; must equal the plain single slab bit for bit.
-    signal 1 (default, depth 5, interior first): consecutive interiors wait for the boundary on
-    the device (slab_wait on the counter the comm stream releases) instead of an event."""
+    The boundary sweeps write the deep halo into the send buffers themselves; order 1 chains
+    back-to-back cycles on one event record per cycle."""
     from cuda_iblb_11_amd import workloads as W
-    monkeypatch.setenv("IBLB_SLAB_SIGNAL", str(signal))
     monkeypatch.setenv("IBLB_RCCL_SELF", "1")
     monkeypatch.setenv("IBLB_OVERLAP", str(overlap))
     monkeypatch.setenv("IBLB_SWEEP_DEPTH", str(depth))
@@ -481,7 +480,6 @@ def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap, order, signal
         assert np.array_equal(r1, r2) and np.array_equal(u1, u2), n
     assert ring.steps == ref.steps == 107
     assert abs(ring.flux - ref.flux) <= 1e-13 * abs(ref.flux)  # per-chunk atomics: order varies
-    ring.synchronize()  # raises if an interior gave up waiting for the boundary signal
     tm = ring.timing()
     if depth == 2:
         assert tm["sweep_launches"] >= 40, tm  # the interior sweeps ran
