@@ -15,6 +15,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -109,9 +111,9 @@ struct iblb_ctx {
     long long sch_t0 = 0;
     // band plans of a schedule: one per cycle from the x coordinates of the cycle's entries
     // (host copies), installed when the cycle's bands differ from the installed ones
-    std::vector<float> sch_x;       // [sch_n][ns]
+    std::vector<float> sch_x;       // [sch_n][ns][2]: point coordinates (x, y) of the schedule
     std::vector<float> sch_x_prev;  // the points before the schedule (their force may be owed)
-    std::vector<std::pair<int, int>> band_b;  // merged forced intervals of the installed plan
+    std::vector<std::array<int, 4>> band_b;  // merged forced patches {x0, x1, y0, y1} of the installed plan
     // pinned host staging of the uploaded tables: a ring, each slot reused only after its copy
     int* band_pin[4] = {nullptr, nullptr, nullptr, nullptr};
     size_t band_pin_cap = 0;  // ints per slot
@@ -127,9 +129,10 @@ struct iblb_ctx {
     bool band_valid = false;
     int* d_band = nullptr;               // level column tables, then the deep sweep table
     size_t band_cap = 0;                 // ints allocated at d_band
-    std::vector<int> band_off, band_n;   // level j = 0 .. K-1: offset / columns in d_band
+    std::vector<int> band_off, band_n;   // level j = 0 .. K-1: offset / entries in d_band
+    std::vector<int> band_nchl;          // level j: chunks per entry (patch rows) launched
     int band_sweep_off = 0, band_nsweep = 0;
-    long long band_deep_cols = 0, band_cols = 0;  // columns of the deep sweep / of all levels
+    long long band_deep_lu = 0, band_lu = 0;  // cells of the deep sweep / of all trapezoid levels
     int band_flux = -1;                  // flux column if a band outputs it, else -1
     char* s_alloc = nullptr;             // two scratch population buffers of the trapezoid
     void* sbuf[2] = {nullptr, nullptr};
@@ -816,6 +819,7 @@ int band_step(iblb_ctx* c) {
     if (c->band_nsweep > 0) {
         Sweep2Args<T> d = sweep_args<T>(c, 0, 1, c->ncol, c->band_nsweep, std::max(1, c->deep_w));
         d.sweep_tab = c->d_band + c->band_sweep_off;
+        d.tab_rows = 1;
         d.vs = c->deep_vs;
         d.variant = c->deep_variant;
         if (d.map == 0) d.map = 2;
@@ -823,7 +827,7 @@ int band_step(iblb_ctx* c) {
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, ds))) return rc;
         HIP_TRY(c, launch_sweepk<T>(d, K, false, ds));
-        if ((rc = ev_end(c, ev, EV_SWEEPK, c->band_deep_cols * c->ny, ds))) return rc;
+        if ((rc = ev_end(c, ev, EV_SWEEPK, c->band_deep_lu, ds))) return rc;
     }
     for (int j = 0; j < K; ++j) {
         const T* src = j == 0 ? A : S[(j - 1) & 1];
@@ -854,6 +858,9 @@ int band_step(iblb_ctx* c) {
         a.col_step = 1;
         a.ncols = c->band_n[j];
         a.nch = c->nch;
+        a.row_tab = 1;
+        a.nchl = c->band_nchl[j];
+        a.store_rows = j == K - 1;  // the last level writes g^{t+K}: patch rows only
         a.flags = c->flags;
         a.fdense = c->fdense;
         a.fplane = c->fplane;
@@ -866,7 +873,7 @@ int band_step(iblb_ctx* c) {
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, bs))) return rc;
         HIP_TRY(c, launch_fused<T>(a, bs));
-        if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * c->ny, bs))) return rc;
+        if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * a.nchl * 64 * c->V, bs))) return rc;
     }
     if (ov) {
         HIP_TRY(c, hipEventRecord(c->ev_b1, ds));
@@ -1378,7 +1385,7 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
 // XCD, two where the band trapezoids hold more than 5 % of the cycle's lattice updates (one-step
 // launches, HBM-bound; the deep sweep is issue-bound).  IBLB_BAND_RESERVE_CUS=0: both on the
 // context's stream, in sequence.
-static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
+static int band_streams(iblb_ctx* c, long long band_lu, long long deep_lu) {
     if (c->transport != TR_NONE || c->comm_stream) return IBLB_OK;  // RCCL groups keep their streams
     if (!c->ncu) {
         hipDeviceProp_t prop;
@@ -1386,7 +1393,7 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
         c->ncu = prop.multiProcessorCount;
     }
     const int per_xcd = std::max(1, c->ncu / 8);
-    const double share = (double)band_cols / (double)std::max(1LL, band_cols + (long long)c->sweep_depth * deep_cols);
+    const double share = (double)band_lu / (double)std::max(1LL, band_lu + (long long)c->sweep_depth * deep_lu);
     long want = env_long("IBLB_BAND_RESERVE_CUS", (share > 0.05 ? 2 : 1) * per_xcd);
     if (want < 0 || want >= c->ncu) want = 0;
     if (want == c->band_reserve || (c->band_sticky && c->band_st)) return IBLB_OK;
@@ -1417,7 +1424,7 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
 // stays false where the cycle does not apply (see band_ready) or does not pay (bands over half
 // the lattice, bands within 2(K-1) columns of the lattice edge: the reference's flat-index wrap).
 template <typename T>
-static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
+static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     const int K = c->sweep_depth, R = 2 * (K - 1);
     // A slab of an RCCL group: local columns, bands and gaps inside [K, ncol-K).  Every rank
     // holds every point and tests every point against its own slab's interior, so all ranks take
@@ -1425,10 +1432,13 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
     const bool slab = !single_slab(c);
     const int nx = slab ? c->ncol : c->nx;  // local columns
     const int lo = slab ? K : 0, hi = slab ? c->ncol - K : c->nx;
-    // forced columns [x0-1, x0+1] of every point, as a column mask
-    std::vector<char> forced((size_t)nx, 0);
-    for (float xv : xs) {
-        double x0 = std::nearbyint((double)xv);
+    const int ny = c->ny;
+    // forced cells of every point: columns [x0-1, x0+1] x rows [y0-1, y0+1] (the 3x3 nodes; rows
+    // outside the lattice receive nothing), as a row range per column
+    std::vector<int> fy0((size_t)nx, INT_MAX), fy1((size_t)nx, INT_MIN);
+    for (size_t k = 0; k + 1 < xy.size(); k += 2) {
+        double x0 = std::nearbyint((double)xy[k]);
+        const int y0 = (int)std::nearbyint((double)xy[k + 1]);
         if (slab) {
             int r = -1;
             for (size_t q = 0; q < c->slab_begin.size(); ++q)
@@ -1444,68 +1454,110 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
             c->band_valid = false;
             return IBLB_OK;
         }
-        for (int x = (int)x0 - 1; x <= (int)x0 + 1; ++x) forced[(size_t)x] = 1;
+        for (int x = (int)x0 - 1; x <= (int)x0 + 1; ++x) {
+            fy0[(size_t)x] = std::min(fy0[(size_t)x], std::max(0, y0 - 1));
+            fy1[(size_t)x] = std::max(fy1[(size_t)x], std::min(ny - 1, y0 + 1));
+        }
     }
-    std::vector<std::pair<int, int>> f;
+    // forced column intervals with their row range, merged into patches {x0, x1, y0, y1} whose
+    // trapezoids stay apart (gaps >= R + 8 columns)
+    std::vector<std::array<int, 4>> b;
     for (int x = 0; x < nx;) {
-        if (!forced[(size_t)x]) { ++x; continue; }
-        int e = x;
-        while (e + 1 < nx && forced[(size_t)e + 1]) ++e;
-        f.push_back({x, e});
-        x = e + 1;
-    }
-    std::sort(f.begin(), f.end());
-    std::vector<std::pair<int, int>> b;  // merged forced intervals: trapezoids apart, gaps >= R + 8
-    for (auto& iv : f) {
-        if (!b.empty() && iv.first - b.back().second - 1 < 2 * R + 8) b.back().second = std::max(b.back().second, iv.second);
-        else b.push_back(iv);
+        if (fy0[(size_t)x] > fy1[(size_t)x]) { ++x; continue; }
+        std::array<int, 4> iv{x, x, fy0[(size_t)x], fy1[(size_t)x]};
+        while (iv[1] + 1 < nx && fy0[(size_t)iv[1] + 1] <= fy1[(size_t)iv[1] + 1]) {
+            ++iv[1];
+            iv[2] = std::min(iv[2], fy0[(size_t)iv[1]]);
+            iv[3] = std::max(iv[3], fy1[(size_t)iv[1]]);
+        }
+        if (!b.empty() && iv[0] - b.back()[1] - 1 < 2 * R + 8) {
+            b.back()[1] = iv[1];
+            b.back()[2] = std::min(b.back()[2], iv[2]);
+            b.back()[3] = std::max(b.back()[3], iv[3]);
+        } else {
+            b.push_back(iv);
+        }
+        x = iv[1] + 1;
     }
     if (c->band_valid && b == c->band_b) return IBLB_OK;  // the installed plan covers these points
     c->band_valid = false;
+    // Rows: a patch's output rows are its forced rows +- (K-1), widened to whole row chunks of
+    // the deep sweep (which advances the rest of the patch's columns); IBLB_BAND_ROWS=0: whole
+    // columns (the trapezoid then covers every row, as before patches)
+    int nchd = 0;
+    (void)sweepk_geometry<T>(K, c->deep_vs, c->deep_variant, false, ny, &nchd);
+    const int vsd = c->deep_vs, gd = (K - 1 + vsd - 1) / vsd, rpc = (64 - 2 * gd) * vsd;  // deep rows per chunk
+    if (nchd <= 0 || (ny + rpc - 1) / rpc != nchd) return IBLB_OK;
+    const bool rows = env_long("IBLB_BAND_ROWS", 1) != 0;
+    const int V64 = 64 * c->V;  // rows per chunk of the one-step kernel
+    std::vector<std::array<int, 4>> pr(b.size());  // per patch: deep chunks [ca, cb), rows [ya, yb)
+    for (size_t q = 0; q < b.size(); ++q) {
+        const int ca = rows ? std::max(0, b[q][2] - (K - 1)) / rpc : 0;
+        const int cb = rows ? std::min(ny - 1, b[q][3] + (K - 1)) / rpc + 1 : nchd;
+        pr[q] = {ca, cb, ca * rpc, std::min(ny, cb * rpc)};
+    }
+    // the trapezoid: level j covers the patch +- (K-1-j) more columns and rows than its output
     std::vector<int> tab;
-    std::vector<int> off((size_t)K), cnt((size_t)K);
-    long long cols = 0;
+    std::vector<int> off((size_t)K), cnt((size_t)K), nchl((size_t)K, 0);
+    long long band_lu = 0;
     for (int j = 0; j < K; ++j) {
         off[j] = (int)tab.size();
-        for (auto& iv : b)
-            for (int x = iv.first - R + j; x <= iv.second + R - j; ++x) tab.push_back(x);
-        cnt[j] = (int)tab.size() - off[j];
-        cols += cnt[j];
+        cnt[j] = 0;
+        const int m = K - 1 - j;
+        for (size_t q = 0; q < b.size(); ++q) {
+            const int ylo = std::max(0, pr[q][2] - m), yhi = std::min(ny, pr[q][3] + m);
+            const int ch0 = ylo / V64, ch1 = std::min(c->nch, (yhi + V64 - 1) / V64);
+            nchl[j] = std::max(nchl[j], ch1 - ch0);
+            for (int x = b[q][0] - R + j; x <= b[q][1] + R - j; ++x) {
+                tab.insert(tab.end(), {x, ch0, ch1, pr[q][2], pr[q][3]});
+                ++cnt[j];
+                band_lu += (long long)(ch1 - ch0) * V64;
+            }
+        }
     }
-    if (!slab && 2 * cols > (long long)K * nx) return IBLB_OK;  // (a slab: the same decision on every rank)
-    // the gaps: columns farther than K-1 from every forced column
-    std::vector<std::pair<int, int>> gaps;
+    if (!slab && 2 * band_lu > (long long)K * nx * ny) return IBLB_OK;  // (a slab: the same decision on every rank)
+    // the deep sweep: every column farther than K-1 from the forced columns (the gaps), and the
+    // patches' output columns outside their rows; regions of (columns, deep chunks)
+    struct Region { int x0, x1, c0, c1; };
+    std::vector<Region> reg;
     int prev = lo;
-    for (auto& iv : b) {
-        if (iv.first - (K - 1) > prev) gaps.push_back({prev, iv.first - (K - 1)});
-        prev = iv.second + K;
+    for (size_t q = 0; q < b.size(); ++q) {
+        const int bx0 = b[q][0] - (K - 1), bx1 = b[q][1] + K;  // output columns [bx0, bx1)
+        if (bx0 > prev) reg.push_back({prev, bx0, 0, nchd});
+        if (pr[q][0] > 0) reg.push_back({bx0, bx1, 0, pr[q][0]});
+        if (pr[q][1] < nchd) reg.push_back({bx0, bx1, pr[q][1], nchd});
+        prev = bx1;
     }
-    if (prev < hi) gaps.push_back({prev, hi});
-    long long ndeep = 0;
-    for (auto& g : gaps) ndeep += g.second - g.first;
-    int rc = band_streams(c, cols, ndeep);
+    if (prev < hi) reg.push_back({prev, hi, 0, nchd});
+    double work = 0.;  // in whole-column equivalents
+    long long deep_lu = 0;
+    for (auto& g : reg) {
+        work += (double)(g.x1 - g.x0) * (g.c1 - g.c0) / nchd;
+        deep_lu += (long long)(g.x1 - g.x0) * std::min(ny, (g.c1 - g.c0) * rpc);
+    }
+    int rc = band_streams(c, band_lu / std::max(1, ny), deep_lu / std::max(1, ny));
     if (rc) return rc;
     // sweeps of ~deep_w columns, balanced to whole rounds of resident waves over the deep
-    // sweep's CUs
+    // sweep's CUs (a sweep over a patch's columns launches every chunk; those of the patch exit)
     const int W = std::max(1, c->deep_w);
     int nch = 0;
     const int wpc = sweepk_geometry<T>(K, c->deep_vs, c->deep_variant, false, c->ny, &nch);
     const int ncu = (slab ? c->ncu - c->reserved_cus : c->ncu - c->band_reserve);
-    long nsw = (long)((ndeep + W - 1) / W);
+    long nsw = (long)std::ceil(work / W);
     const long slots = (long)wpc * ncu;
-    if (c->deep_balance && slots > 0 && nch > 0 && ndeep > 0) {
+    if (c->deep_balance && slots > 0 && nch > 0 && work > 0.) {
         const long rounds = std::max(1L, (nsw * nch + slots / 2) / slots);
         nsw = std::max(1L, rounds * slots / nch);
     }
     const int sweep_off = (int)tab.size();
     int nsweep = 0;
-    for (auto& g : gaps) {
-        const long w = g.second - g.first;
-        long n = std::max(1L, std::lround((double)nsw * (double)w / (double)ndeep));
+    for (auto& g : reg) {
+        const long w = g.x1 - g.x0;
+        const double share = (double)w * (g.c1 - g.c0) / nchd / std::max(work, 1e-9);
+        long n = std::max(1L, std::lround((double)nsw * share));
         n = std::min(n, w);
         for (long k = 0; k < n; ++k) {
-            tab.push_back(g.first + (int)(k * w / n));
-            tab.push_back(g.first + (int)((k + 1) * w / n));
+            tab.insert(tab.end(), {g.x0 + (int)(k * w / n), g.x0 + (int)((k + 1) * w / n), g.c0, g.c1});
             ++nsweep;
         }
     }
@@ -1514,7 +1566,7 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
         if (c->d_band) (void)hipFree(c->d_band);
         c->d_band = nullptr;
         c->band_cap = 0;
-        const size_t cap = std::max(tab.size(), (size_t)(K + 1) * nx + 4 * (size_t)nsw + 64);
+        const size_t cap = std::max(tab.size(), (size_t)5 * (K + 1) * nx + 8 * (size_t)nsw + 64);
         HIP_TRY(c, hipMalloc(&c->d_band, cap * sizeof(int)));
         c->band_cap = cap;
     }
@@ -1552,18 +1604,19 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xs) {
     c->band_n = cnt;
     c->band_sweep_off = sweep_off;
     c->band_nsweep = nsweep;
-    c->band_deep_cols = ndeep;
-    c->band_cols = cols;
+    c->band_nchl = nchl;
+    c->band_deep_lu = deep_lu;
+    c->band_lu = band_lu;
     c->band_flux = -1;
     const int fc = c->cfg.flux_column - (slab ? c->x_begin : 0);
     for (auto& iv : b)
-        if (fc >= iv.first - (K - 1) && fc <= iv.second + (K - 1)) c->band_flux = fc;
+        if (fc >= iv[0] - (K - 1) && fc <= iv[1] + (K - 1)) c->band_flux = fc;
     c->band_b = b;
     c->band_valid = true;
     return IBLB_OK;
 }
 
-static int plan_bands(iblb_ctx* c, const std::vector<float>& xs) {
+static int plan_bands(iblb_ctx* c, const std::vector<float>& xs) {  // (x, y) pairs
     if (!c->band_on || xs.empty() || c->sweep_depth < 3 || !c->sweep_on || !(single_slab(c) || band_slab_ok(c)) ||
         c->cilia_on) {
         c->band_valid = false;
@@ -1578,21 +1631,19 @@ static int plan_bands(iblb_ctx* c, const std::vector<float>& xs) {
 static int plan_cycle(iblb_ctx* c) {
     const int K = c->sweep_depth, ns = c->ns;
     std::vector<float> xs;
-    xs.reserve((size_t)(K + 1) * ns);
+    xs.reserve((size_t)(K + 1) * 2 * ns);
     for (long long it = c->t - 1; it <= c->t + K - 2; ++it) {
         if (it < c->sch_t0) {
             xs.insert(xs.end(), c->sch_x_prev.begin(), c->sch_x_prev.end());
             continue;
         }
         const size_t e = (size_t)sched_entry(c, it);
-        xs.insert(xs.end(), c->sch_x.begin() + e * ns, c->sch_x.begin() + (e + 1) * ns);
+        xs.insert(xs.end(), c->sch_x.begin() + e * 2 * ns, c->sch_x.begin() + (e + 1) * 2 * ns);
     }
     return plan_bands(c, xs);
 }
-static std::vector<float> x_coords(int ns, const float* s) {
-    std::vector<float> xs((size_t)ns);
-    for (int k = 0; k < ns; ++k) xs[(size_t)k] = s[2 * k];
-    return xs;
+static std::vector<float> x_coords(int ns, const float* s) {  // (x, y) of every point
+    return std::vector<float>(s, s + 2 * (size_t)ns);
 }
 
 extern "C" {

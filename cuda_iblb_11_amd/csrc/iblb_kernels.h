@@ -36,6 +36,14 @@ struct FusedArgs {
     Coef c;
     KConst k;           // collide constants folded on the host (iblb_device.h)
     int variant;        // kernel variant (MODE bits of lbm_kernels.hip), 0 = default
+    // IB band patches (band cycle, rows restricted): with row_tab set, cols holds 5 ints per entry
+    // from col_begin on, {column, first chunk, end chunk, first row, end row}, and launch entry e
+    // covers chunks [first, end) of its column (nchl waves per entry, the extra ones exit).  Q is
+    // sampled on rows [first row, end row) only; store_rows: the populations too (other rows of
+    // the column belong to the deep sweep).
+    int row_tab = 0;
+    int nchl = 0;
+    int store_rows = 0;
 };
 
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.
@@ -82,6 +90,8 @@ struct Sweep2Args {
     int xcds;            // deep sweeps, map 2: XCDs the workgroups are dealt over (0 = 8)
     const int* sweep_tab;  // deep sweeps: sweep s covers [sweep_tab[2s], sweep_tab[2s+1]) (device;
                            // nullptr: col_begin / col_step / W); the force-free gaps between IB bands
+    int tab_rows;          // sweep_tab entries of 4 ints: + chunk range [tab[4s+2], tab[4s+3]) of the
+                           // sweep (the columns of an IB band outside its patch rows)
     int flux_col;        // local column sampled for Q (both iterations), or -1
     double flux_norm;
     double* Q;

@@ -20,10 +20,21 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
     constexpr bool DEV = Store<T>::dev;
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (gw >= a.ncols * a.nch) return;
-    const int xc = a.cols ? __builtin_amdgcn_readfirstlane(a.cols[a.col_begin + gw / a.nch])
-                          : a.col_begin + (gw / a.nch) * a.col_step;
-    const int ch = gw - (gw / a.nch) * a.nch;
+    int xc, ch, ya = 0, yb = a.L.rows;  // rows sampled for Q (and stored, store_rows)
+    if (a.row_tab) {  // an IB patch entry: chunks [e[1], e[2]) of column e[0]
+        if (gw >= a.ncols * a.nchl) return;
+        const int* e = a.cols + a.col_begin + 5 * (gw / a.nchl);
+        ch = __builtin_amdgcn_readfirstlane(e[1]) + gw % a.nchl;
+        if (ch >= __builtin_amdgcn_readfirstlane(e[2])) return;
+        xc = __builtin_amdgcn_readfirstlane(e[0]);
+        ya = __builtin_amdgcn_readfirstlane(e[3]);
+        yb = __builtin_amdgcn_readfirstlane(e[4]);
+    } else {
+        if (gw >= a.ncols * a.nch) return;
+        xc = a.cols ? __builtin_amdgcn_readfirstlane(a.cols[a.col_begin + gw / a.nch])
+                    : a.col_begin + (gw / a.nch) * a.col_step;
+        ch = gw - (gw / a.nch) * a.nch;
+    }
     const Layout L = a.L;
     const int cs = ch * (64 * V);
     const int y0 = cs + lane * V;
@@ -92,20 +103,30 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
         // body force only: the host-folded constants; with an IB force: the same fold per cell
         const R ux = (IB && has_f) ? relax_cell<R, DEV>(f, kb, make_kforce<R>(kb, (R)(a.c.gx + fxv[e]), (R)(a.c.gy + fyv[e])))
                                    : relax_cell<R, DEV>(f, kb, kbody<R>(a.k));
-        if (do_flux && y0 + e < L.ny) q += (double)ux / a.flux_norm;
+        if (do_flux && y0 + e < L.ny && y0 + e >= ya && y0 + e < yb) q += (double)ux / a.flux_norm;
         v0[e] = (T)f[0]; v1[e] = (T)f[1]; v2[e] = (T)f[2]; v3[e] = (T)f[3]; v4[e] = (T)f[4];
         v5[e] = (T)f[5]; v6[e] = (T)f[6]; v7[e] = (T)f[7]; v8[e] = (T)f[8];
     }
     T* dst = a.dst + cb + y0;
-    st_plane<T, V, MODE>(dst, v0);
-    st_plane<T, V, MODE>(dst + 1 * L.plane, v1);
-    st_plane<T, V, MODE>(dst + 2 * L.plane, v2);
-    st_plane<T, V, MODE>(dst + 3 * L.plane, v3);
-    st_plane<T, V, MODE>(dst + 4 * L.plane, v4);
-    st_plane<T, V, MODE>(dst + 5 * L.plane, v5);
-    st_plane<T, V, MODE>(dst + 6 * L.plane, v6);
-    st_plane<T, V, MODE>(dst + 7 * L.plane, v7);
-    st_plane<T, V, MODE>(dst + 8 * L.plane, v8);
+    if (!a.store_rows || (y0 >= ya && y0 + V <= yb)) {
+        st_plane<T, V, MODE>(dst, v0);
+        st_plane<T, V, MODE>(dst + 1 * L.plane, v1);
+        st_plane<T, V, MODE>(dst + 2 * L.plane, v2);
+        st_plane<T, V, MODE>(dst + 3 * L.plane, v3);
+        st_plane<T, V, MODE>(dst + 4 * L.plane, v4);
+        st_plane<T, V, MODE>(dst + 5 * L.plane, v5);
+        st_plane<T, V, MODE>(dst + 6 * L.plane, v6);
+        st_plane<T, V, MODE>(dst + 7 * L.plane, v7);
+        st_plane<T, V, MODE>(dst + 8 * L.plane, v8);
+    } else if (y0 + V > ya && y0 < yb) {  // a lane across the patch's first or last row
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+            if (y0 + e >= ya && y0 + e < yb) {
+                dst[e] = v0[e]; dst[e + 1 * L.plane] = v1[e]; dst[e + 2 * L.plane] = v2[e];
+                dst[e + 3 * L.plane] = v3[e]; dst[e + 4 * L.plane] = v4[e]; dst[e + 5 * L.plane] = v5[e];
+                dst[e + 6 * L.plane] = v6[e]; dst[e + 7 * L.plane] = v7[e]; dst[e + 8 * L.plane] = v8[e];
+            }
+    }
     if (xc == 0 && a.send_left[0]) {
         sta<T, V>(a.send_left[0] + y0, v3);
         sta<T, V>(a.send_left[1] + y0, v6);
@@ -134,7 +155,7 @@ hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t
 
 template <typename T>
 hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s) {
-    const long waves = (long)a.ncols * a.nch;
+    const long waves = (long)a.ncols * (a.row_tab ? a.nchl : a.nch);
     if (waves <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     switch (a.variant) {

@@ -609,7 +609,12 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     linear_item(a.map, a.nch, a.xcds, wv, sw, ch);
     if (sw >= a.nsweep || ch >= a.nch) return;
     int xa, xb;
-    if (a.sweep_tab) {
+    if (a.sweep_tab && a.tab_rows) {
+        const int* e = a.sweep_tab + 4 * sw;
+        if (ch < e[2] || ch >= e[3]) return;  // wave-uniform: rows of an IB patch
+        xa = __builtin_amdgcn_readfirstlane(e[0]);
+        xb = __builtin_amdgcn_readfirstlane(e[1]);
+    } else if (a.sweep_tab) {
         xa = __builtin_amdgcn_readfirstlane(a.sweep_tab[2 * sw]);
         xb = __builtin_amdgcn_readfirstlane(a.sweep_tab[2 * sw + 1]);
     } else if (a.col_step > 0) {
