@@ -134,6 +134,11 @@ struct iblb_ctx {
     int band_sweep_off = 0, band_nsweep = 0;
     long long band_deep_lu = 0, band_lu = 0;  // cells of the deep sweep / of all trapezoid levels
     int band_flux = -1;                  // flux column if a band outputs it, else -1
+    // the band chain as ONE launch (band_kernel: a workgroup per patch runs its whole trapezoid,
+    // IB included; IBLB_BAND_FUSED=1) instead of 2K dependent launches (default: one workgroup
+    // per patch is latency-bound, K3 0.25 vs 0.09 ms per cycle, profiles/r02ad)
+    int band_fused = 0;
+    int band_npatch = 0, band_pt_off = 0;  // patches; their table in d_band (BAND_PT ints each)
     char* s_alloc = nullptr;             // two scratch population buffers of the trapezoid
     void* sbuf[2] = {nullptr, nullptr};
     long buf_elems = 0, buf_gap = 0;
@@ -765,6 +770,11 @@ bool band_ready(const iblb_ctx* c) {
 }
 
 template <typename T>
+int band_deep(iblb_ctx* c, int K, hipStream_t ds);
+template <typename T>
+int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool slab, hipStream_t bs, hipStream_t ds);
+
+template <typename T>
 int band_step(iblb_ctx* c) {
     const int K = c->sweep_depth;
     int rc;
@@ -781,7 +791,7 @@ int band_step(iblb_ctx* c) {
     // (none reads the halo); the comm stream exchanges the deep halo and advances the force-free
     // boundary columns [0, K), [ncol-K, ncol) exactly as deep_slab_step does.
     const bool slab = !single_slab(c);
-    const bool ov = c->band_st != nullptr && !slab;
+    const bool ov = c->band_st != nullptr && (!slab || c->band_fused);
     hipStream_t bs = ov ? c->band_st : c->stream, ds = ov ? c->deep_st : c->stream;
     if (slab) {
         if ((rc = join_comm(c))) return rc;  // boundary(t-K) wrote columns the interior reads
@@ -798,6 +808,113 @@ int band_step(iblb_ctx* c) {
         HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_b0, 0));
         HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_b0, 0));
     }
+    if (c->band_fused) {
+        // the deep sweep over the gaps, beside ONE band-kernel launch for every patch's trapezoid
+        if ((rc = band_deep<T>(c, K, ds))) return rc;
+        BandArgs<T> ba{};
+        FusedArgs<T>& a = ba.f;
+        a.L = c->L;
+        for (int p = 0; p < 3; ++p) a.send_left[p] = a.send_right[p] = nullptr;
+        a.cols = c->d_band;
+        a.nch = c->nch;
+        a.row_tab = 1;
+        a.flags = c->flags;
+        a.fdense = c->fdense;
+        a.fplane = c->fplane;
+        a.flux_col = c->band_flux;  // ghost columns of the trapezoid never add flux
+        a.flux_norm = c->cfg.flux_norm;
+        a.Q = c->d_Q;
+        a.c = c->coef;
+        a.k = c->kc;
+        a.variant = c->variant;
+        for (int j = 0; j < K; ++j) {
+            ba.src[j] = j == 0 ? A : S[(j - 1) & 1];
+            ba.dst[j] = j == K - 1 ? B : S[j & 1];
+            // level j's points: those of iteration t+j-1 (j = 0: the current ones, whose force is owed)
+            ba.ps[j] = j == 0 ? pts_s(c) : c->d_s;
+            ba.pus[j] = j == 0 ? pts_us(c) : c->d_us;
+            ba.pe[j] = j == 0 ? pts_eps(c) : c->d_eps;
+            if (j > 0 && c->sch_n > 0) {
+                const int e = sched_entry(c, c->t + j - 1);
+                ba.ps[j] = sched_ptr(c->d_sch_s, c, e, 2);
+                ba.pus[j] = sched_ptr(c->d_sch_us, c, e, 2);
+                ba.pe[j] = sched_ptr(c->d_sch_eps, c, e, 1);
+            }
+        }
+        ba.H0 = halo_at<T>(c, A);
+        ba.pt = c->d_band + c->band_pt_off;
+        ba.npatch = c->band_npatch;
+        ba.K = K;
+        ba.ib0 = c->ib_state == IB_PENDING;
+        ba.ns = c->ns;
+        ba.nx = c->nx;
+        ba.x_begin = c->x_begin;
+        ba.slab = slab;
+        ba.X = IbHalo<T>{(const T*)c->recv_left, (const T*)c->recv_right};
+        ba.F_s = c->d_Fs;
+        ba.rows_per_chunk = 64 * c->V;
+        size_t ev = 0;
+        if ((rc = ev_begin(c, &ev, bs))) return rc;
+        HIP_TRY(c, launch_band<T>(ba, bs));
+        if ((rc = ev_end(c, ev, EV_FUSED, c->band_lu, bs))) return rc;
+        c->ib_state = IB_READY;
+    } else if ((rc = band_chain<T>(c, K, A, B, S, slab, bs, ds))) {
+        return rc;
+    }
+    if (ov) {
+        HIP_TRY(c, hipEventRecord(c->ev_b1, ds));
+        HIP_TRY(c, hipEventRecord(c->ev_b2, bs));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b1, 0));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b2, 0));
+    }
+    if (slab) {
+        // comm: deep halo exchange(t) -> (after the compute work before this cycle, which read
+        // the columns the boundary sweeps overwrite) boundary sweeps -> deep halo of g^{t+K}
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        hipStream_t cs = c->comm_stream;
+        if ((rc = exchange_rccl(c, cs, false, false, deep_slots(K)))) return rc;
+        HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_pre, 0));
+        Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
+        b.vs = c->deep_bnd_vs;
+        b.variant = c->deep_variant;
+        if (b.map == 0) b.map = 2;
+        HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));  // also packs the deep halo of B
+        HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));
+        c->send_sweep = false;
+        c->send_deep = K;
+    }
+    c->cur = 1 - c->cur;
+    c->t += K;
+    c->halo_valid = false;
+    c->ib_state = IB_PENDING;
+    // the force now owed is that of iteration t+K-1's points
+    return c->sch_n > 0 ? sched_use(c, sched_entry(c, c->t - 1)) : IBLB_OK;
+}
+
+// the deep sweep of a band cycle over the force-free gaps (and the band columns outside the
+// patch rows): the sweep table of the plan
+template <typename T>
+int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
+    if (c->band_nsweep <= 0) return IBLB_OK;
+    Sweep2Args<T> d = sweep_args<T>(c, 0, 1, c->ncol, c->band_nsweep, std::max(1, c->deep_w));
+    d.sweep_tab = c->d_band + c->band_sweep_off;
+    d.tab_rows = 1;
+    d.vs = c->deep_vs;
+    d.variant = c->deep_variant;
+    if (d.map == 0) d.map = 2;
+    d.xcds = (int)env_long("IBLB_DEEP_XCDS", 0);  // eight: masks take CUs of every XCD (interior above)
+    size_t ev = 0;
+    int rc = ev_begin(c, &ev, ds);
+    if (rc) return rc;
+    HIP_TRY(c, launch_sweepk<T>(d, K, false, ds));
+    return ev_end(c, ev, EV_SWEEPK, c->band_deep_lu, ds);
+}
+
+// The band chain as 2K dependent launches (IBLB_BAND_FUSED=0): the IB of each level over every
+// point, then the level's one-step launch over the trapezoid's entries.
+template <typename T>
+int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool slab, hipStream_t bs, hipStream_t ds) {
+    int rc;
     // IB of one level: a lone slab with every point; a group slab with the points spreading into
     // it (all inner: no halo is read) and zero F_s for the others
     IbHalo<T> X{(const T*)c->recv_left, (const T*)c->recv_right};
@@ -816,19 +933,7 @@ int band_step(iblb_ctx* c) {
         c->ib_state = IB_READY;
     }
     // deep sweep over the force-free gaps first: the chip is full while it runs
-    if (c->band_nsweep > 0) {
-        Sweep2Args<T> d = sweep_args<T>(c, 0, 1, c->ncol, c->band_nsweep, std::max(1, c->deep_w));
-        d.sweep_tab = c->d_band + c->band_sweep_off;
-        d.tab_rows = 1;
-        d.vs = c->deep_vs;
-        d.variant = c->deep_variant;
-        if (d.map == 0) d.map = 2;
-        d.xcds = (int)env_long("IBLB_DEEP_XCDS", 0);  // eight: masks take CUs of every XCD (interior above)
-        size_t ev = 0;
-        if ((rc = ev_begin(c, &ev, ds))) return rc;
-        HIP_TRY(c, launch_sweepk<T>(d, K, false, ds));
-        if ((rc = ev_end(c, ev, EV_SWEEPK, c->band_deep_lu, ds))) return rc;
-    }
+    if ((rc = band_deep<T>(c, K, ds))) return rc;
     for (int j = 0; j < K; ++j) {
         const T* src = j == 0 ? A : S[(j - 1) & 1];
         T* dst = j == K - 1 ? B : S[j & 1];
@@ -875,34 +980,7 @@ int band_step(iblb_ctx* c) {
         HIP_TRY(c, launch_fused<T>(a, bs));
         if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * a.nchl * 64 * c->V, bs))) return rc;
     }
-    if (ov) {
-        HIP_TRY(c, hipEventRecord(c->ev_b1, ds));
-        HIP_TRY(c, hipEventRecord(c->ev_b2, bs));
-        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b1, 0));
-        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b2, 0));
-    }
-    if (slab) {
-        // comm: deep halo exchange(t) -> (after the compute work before this cycle, which read
-        // the columns the boundary sweeps overwrite) boundary sweeps -> deep halo of g^{t+K}
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
-        hipStream_t cs = c->comm_stream;
-        if ((rc = exchange_rccl(c, cs, false, false, deep_slots(K)))) return rc;
-        HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_pre, 0));
-        Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
-        b.vs = c->deep_bnd_vs;
-        b.variant = c->deep_variant;
-        if (b.map == 0) b.map = 2;
-        HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));  // also packs the deep halo of B
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));
-        c->send_sweep = false;
-        c->send_deep = K;
-    }
-    c->cur = 1 - c->cur;
-    c->t += K;
-    c->halo_valid = false;
-    c->ib_state = IB_PENDING;
-    // the force now owed is that of iteration t+K-1's points
-    return c->sch_n > 0 ? sched_use(c, sched_entry(c, c->t - 1)) : IBLB_OK;
+    return IBLB_OK;
 }
 
 template <typename T>
@@ -1246,6 +1324,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
         c->buf_gap = gap;
     }
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
+    c->band_fused = (int)env_long("IBLB_BAND_FUSED", 0);
     // halo buffers: recv_left, recv_right, send_left, send_right; each 10 (2-step) or 21 (IB)
     // slots + guards
     {
@@ -1377,25 +1456,44 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
 
 }  // extern "C"
 
-// Streams of the overlapped band cycle (lone slab): the band chain on band_st restricted to
-// `band_reserve` CUs (the top mask bits, like the RCCL comm stream's: bit i is a CU of XCD i % 8,
-// so 32 bits are four CUs of every XCD, profiles/r02n_xcc_probe.txt), the cycle's deep sweep on
-// deep_st masked to the other CUs.  The context's stream is never replaced: it keeps the
-// whole chip for every other launch and joins the two with events in band_step.  Default: one
-// XCD, two where the band trapezoids hold more than 5 % of the cycle's lattice updates (one-step
-// launches, HBM-bound; the deep sweep is issue-bound).  IBLB_BAND_RESERVE_CUS=0: both on the
-// context's stream, in sequence.
-static int band_streams(iblb_ctx* c, long long band_lu, long long deep_lu) {
-    if (c->transport != TR_NONE || c->comm_stream) return IBLB_OK;  // RCCL groups keep their streams
+// Streams of the overlapped band cycle: the band chain on band_st restricted to `band_reserve`
+// CUs (the top mask bits of the CUs the cycle may use: bit i is a CU of XCD i % 8, so 8m bits are
+// m CUs of every XCD, profiles/r02n_xcc_probe.txt), the cycle's deep sweep on deep_st masked to
+// the others.  A lone slab may use the whole chip; a slab of an RCCL group the compute stream's
+// CUs (comp_mask: the comm stream keeps its reserved CUs for the exchange and the boundary
+// sweeps).  The context's stream is never replaced: it keeps its CUs for every other launch and
+// joins the two with events in band_step.  Defaults: the fused band kernel (one workgroup per
+// patch) gets 8 * ceil(patches / (8 * IBLB_BAND_ROUNDS)) CUs (rounds of one workgroup per CU);
+// the launch-per-level chain one XCD's worth, two where the trapezoids hold more than 5 % of the
+// cycle's lattice updates (one-step launches, HBM-bound; the deep sweep is issue-bound).
+// IBLB_BAND_RESERVE_CUS overrides; 0: both on the context's stream, in sequence.
+static int band_streams(iblb_ctx* c, long long band_lu, long long deep_lu, int npatch) {
+    const bool slab = rccl_multi(c);
+    if (c->transport == TR_LOCAL || (!slab && c->comm_stream) || (slab && !c->band_fused)) return IBLB_OK;
     if (!c->ncu) {
         hipDeviceProp_t prop;
         HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
         c->ncu = prop.multiProcessorCount;
     }
     const int per_xcd = std::max(1, c->ncu / 8);
-    const double share = (double)band_lu / (double)std::max(1LL, band_lu + (long long)c->sweep_depth * deep_lu);
-    long want = env_long("IBLB_BAND_RESERVE_CUS", (share > 0.05 ? 2 : 1) * per_xcd);
-    if (want < 0 || want >= c->ncu) want = 0;
+    long dflt;
+    if (c->band_fused) {
+        const long rounds = std::max(1L, env_long("IBLB_BAND_ROUNDS", 2));
+        dflt = 8 * ((npatch + 8 * rounds - 1) / (8 * rounds));
+    } else {
+        const double share = (double)band_lu / (double)std::max(1LL, band_lu + (long long)c->sweep_depth * deep_lu);
+        dflt = (share > 0.05 ? 2 : 1) * per_xcd;
+    }
+    // the CUs the cycle may use
+    std::vector<uint32_t> base((size_t)(c->ncu + 31) / 32, 0u);
+    int avail = 0;
+    for (int i = 0; i < c->ncu; ++i)
+        if (!slab || c->comp_mask.empty() || (c->comp_mask[(size_t)i / 32] >> (i % 32) & 1u)) {
+            base[(size_t)i / 32] |= 1u << (i % 32);
+            ++avail;
+        }
+    long want = env_long("IBLB_BAND_RESERVE_CUS", dflt);
+    if (want < 0 || want >= avail) want = 0;
     if (want == c->band_reserve || (c->band_sticky && c->band_st)) return IBLB_OK;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     for (hipStream_t* st : {&c->band_st, &c->deep_st})
@@ -1405,10 +1503,13 @@ static int band_streams(iblb_ctx* c, long long band_lu, long long deep_lu) {
             *st = nullptr;
         }
     if (want) {
-        std::vector<uint32_t> deep((size_t)(c->ncu + 31) / 32, 0u), band(deep.size(), 0u);
-        for (int i = 0; i < c->ncu; ++i) {
-            std::vector<uint32_t>& m = i >= c->ncu - want ? band : deep;
+        std::vector<uint32_t> deep(base.size(), 0u), band(base.size(), 0u);
+        long taken = 0;
+        for (int i = c->ncu - 1; i >= 0; --i) {
+            if (!(base[(size_t)i / 32] >> (i % 32) & 1u)) continue;
+            std::vector<uint32_t>& m = taken < want ? band : deep;
             m[(size_t)i / 32] |= 1u << (i % 32);
+            ++taken;
         }
         HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->deep_st, (uint32_t)deep.size(), deep.data()));
         HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->band_st, (uint32_t)band.size(), band.data()));
@@ -1454,9 +1555,12 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
             c->band_valid = false;
             return IBLB_OK;
         }
+        // (clamped into the lattice: a point whose nodes all miss it still gets a patch, so the
+        // fused band kernel, which lists points by patch, writes its F_s)
+        const int ya = std::min(std::max(0, y0 - 1), ny - 1), yb = std::max(std::min(ny - 1, y0 + 1), 0);
         for (int x = (int)x0 - 1; x <= (int)x0 + 1; ++x) {
-            fy0[(size_t)x] = std::min(fy0[(size_t)x], std::max(0, y0 - 1));
-            fy1[(size_t)x] = std::max(fy1[(size_t)x], std::min(ny - 1, y0 + 1));
+            fy0[(size_t)x] = std::min(fy0[(size_t)x], std::min(ya, yb));
+            fy1[(size_t)x] = std::max(fy1[(size_t)x], std::max(ya, yb));
         }
     }
     // forced column intervals with their row range, merged into patches {x0, x1, y0, y1} whose
@@ -1499,6 +1603,13 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     // the trapezoid: level j covers the patch +- (K-1-j) more columns and rows than its output
     std::vector<int> tab;
     std::vector<int> off((size_t)K), cnt((size_t)K), nchl((size_t)K, 0);
+    // the fused band kernel's patch table (BandArgs::pt): x0 range of the patch's points, then per
+    // level {first entry (ints into d_band), entries, chunks per entry}
+    std::vector<int> ptab(b.size() * BAND_PT, 0);
+    for (size_t q = 0; q < b.size(); ++q) {
+        ptab[q * BAND_PT + 0] = b[q][0] + 1;
+        ptab[q * BAND_PT + 1] = b[q][1] - 1;
+    }
     long long band_lu = 0;
     for (int j = 0; j < K; ++j) {
         off[j] = (int)tab.size();
@@ -1508,6 +1619,9 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
             const int ylo = std::max(0, pr[q][2] - m), yhi = std::min(ny, pr[q][3] + m);
             const int ch0 = ylo / V64, ch1 = std::min(c->nch, (yhi + V64 - 1) / V64);
             nchl[j] = std::max(nchl[j], ch1 - ch0);
+            ptab[q * BAND_PT + 2 + 3 * j] = (int)tab.size();
+            ptab[q * BAND_PT + 3 + 3 * j] = b[q][1] - b[q][0] + 1 + 2 * (R - j);
+            ptab[q * BAND_PT + 4 + 3 * j] = ch1 - ch0;
             for (int x = b[q][0] - R + j; x <= b[q][1] + R - j; ++x) {
                 tab.insert(tab.end(), {x, ch0, ch1, pr[q][2], pr[q][3]});
                 ++cnt[j];
@@ -1535,14 +1649,14 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
         work += (double)(g.x1 - g.x0) * (g.c1 - g.c0) / nchd;
         deep_lu += (long long)(g.x1 - g.x0) * std::min(ny, (g.c1 - g.c0) * rpc);
     }
-    int rc = band_streams(c, band_lu / std::max(1, ny), deep_lu / std::max(1, ny));
+    int rc = band_streams(c, band_lu / std::max(1, ny), deep_lu / std::max(1, ny), (int)b.size());
     if (rc) return rc;
     // sweeps of ~deep_w columns, balanced to whole rounds of resident waves over the deep
     // sweep's CUs (a sweep over a patch's columns launches every chunk; those of the patch exit)
     const int W = std::max(1, c->deep_w);
     int nch = 0;
     const int wpc = sweepk_geometry<T>(K, c->deep_vs, c->deep_variant, false, c->ny, &nch);
-    const int ncu = (slab ? c->ncu - c->reserved_cus : c->ncu - c->band_reserve);
+    const int ncu = (slab ? c->ncu - c->reserved_cus : c->ncu) - c->band_reserve;
     long nsw = (long)std::ceil(work / W);
     const long slots = (long)wpc * ncu;
     if (c->deep_balance && slots > 0 && nch > 0 && work > 0.) {
@@ -1561,6 +1675,8 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
             ++nsweep;
         }
     }
+    const int pt_off = (int)tab.size();
+    tab.insert(tab.end(), ptab.begin(), ptab.end());
     if (tab.size() > c->band_cap) {  // grow (rare: sized for the whole lattice at K+1 levels)
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         if (c->d_band) (void)hipFree(c->d_band);
@@ -1604,6 +1720,8 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     c->band_n = cnt;
     c->band_sweep_off = sweep_off;
     c->band_nsweep = nsweep;
+    c->band_pt_off = pt_off;
+    c->band_npatch = (int)b.size();
     c->band_nchl = nchl;
     c->band_deep_lu = deep_lu;
     c->band_lu = band_lu;

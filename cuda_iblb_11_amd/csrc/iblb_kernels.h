@@ -46,6 +46,42 @@ struct FusedArgs {
     int store_rows = 0;
 };
 
+// The band chain of one IB band cycle in ONE launch (lbm_kernels.hip band_kernel): workgroup q
+// runs patch q's whole trapezoid, level j = 0 .. K-1: the IB of the level's points whose node
+// column x0 lies in the patch (force^{t+j} from level j-1, or from g^t at j = 0 when owed), a
+// workgroup barrier, the one-step collide of the level's entries (fused_wave), a barrier.  The
+// patches' columns are disjoint and apart, so workgroups never share a cell, a force value or a
+// flag.  Bit-identical to the launch-per-level chain (same bodies, same data; spread atomics in
+// another order).
+constexpr int BAND_MAX_K = 6;
+constexpr int BAND_PT = 2 + 3 * BAND_MAX_K;  // ints per patch in the patch table
+template <typename T>
+struct BandArgs {
+    FusedArgs<T> f;                  // the collide arguments common to every level (cols = the
+                                     // entry table, row_tab = 1); src / dst / H / entries per level
+    const T* src[BAND_MAX_K];        // level j reads src[j] (g^t, then the scratch levels) ...
+    T* dst[BAND_MAX_K];              // ... and writes dst[j] (the last level: g^{t+K}, patch rows)
+    Halo<T> H0;                      // periodic images of g^t (the only level that can reach x = 0)
+    // patch q: pt[q*BAND_PT + 0..1] = the x0 range [lo, hi] (local) of its points, then per level
+    // j: {first entry, entries, chunks per entry} at pt[q*BAND_PT + 2 + 3j]
+    const int* pt;
+    int npatch;
+    int K;
+    int ib0;                         // level 0 evaluates force^t from g^t (owed)
+    const float* ps[BAND_MAX_K];     // the points of level j (iteration t+j-1; j = 0: the current)
+    const float* pus[BAND_MAX_K];
+    const int* pe[BAND_MAX_K];
+    int ns;
+    int nx;
+    int x_begin;
+    int slab;                        // a slab of a group: IB by ib_slab_group (no halo is reached)
+    IbHalo<T> X;
+    float* F_s;
+    int rows_per_chunk;              // of the IB flags (64 * V)
+};
+template <typename T>
+hipError_t launch_band(const BandArgs<T>& a, hipStream_t s);
+
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.
 // 2-step halo of a slab (SWEEP_HALO_SLOTS slots of L.rows elements per side):
 //   from the left  neighbour: 0-2 col -1 {1,5,8}, 3-5 col -1 {0,2,4}, 6-8 col -2 {1,5,8},

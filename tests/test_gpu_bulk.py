@@ -264,13 +264,16 @@ def test_band_streams_keep_the_context_stream(gpu, monkeypatch):
     assert rel(r1, r2) <= 1e-13 and rel(u1, u2) <= 1e-12
 
 
-@pytest.mark.parametrize("precision", ["f64", "f32"])
-def test_rccl_self_ring_ib_band_cycle(gpu, monkeypatch, precision):
+@pytest.mark.parametrize("precision,fused", [("f64", 1), ("f32", 1), ("f64", 0)])
+def test_rccl_self_ring_ib_band_cycle(gpu, monkeypatch, precision, fused):
     """The IB band cycle of a slab group over REAL RCCL (one rank, its own neighbour): moving
     filaments inside the slab, points given ahead, bulk calls with readers between them; equals
-    the lone slab (same band cycle without halos) up to the spread atomics' order."""
+    the lone slab (same band cycle without halos) up to the spread atomics' order.  fused: the
+    band chain as one launch on its own CU-masked stream beside the deep sweep (default), or the
+    2K-launch chain on the compute stream."""
     from cuda_iblb_11_amd import workloads as W
     monkeypatch.setenv("IBLB_RCCL_SELF", "1")
+    monkeypatch.setenv("IBLB_BAND_FUSED", str(fused))
     nx, ny = 256, 128
     pts = _swaying(nx, n_fil=2, pts=40)
     rho, u = W.perturbed_state(nx, ny, 17)
