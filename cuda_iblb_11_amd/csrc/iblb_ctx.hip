@@ -791,7 +791,7 @@ int band_step(iblb_ctx* c) {
     // (none reads the halo); the comm stream exchanges the deep halo and advances the force-free
     // boundary columns [0, K), [ncol-K, ncol) exactly as deep_slab_step does.
     const bool slab = !single_slab(c);
-    const bool ov = c->band_st != nullptr && (!slab || c->band_fused);
+    const bool ov = c->band_st != nullptr;
     hipStream_t bs = ov ? c->band_st : c->stream, ds = ov ? c->deep_st : c->stream;
     if (slab) {
         if ((rc = join_comm(c))) return rc;  // boundary(t-K) wrote columns the interior reads
@@ -1469,7 +1469,8 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
 // IBLB_BAND_RESERVE_CUS overrides; 0: both on the context's stream, in sequence.
 static int band_streams(iblb_ctx* c, long long band_lu, long long deep_lu, int npatch) {
     const bool slab = rccl_multi(c);
-    if (c->transport == TR_LOCAL || (!slab && c->comm_stream) || (slab && !c->band_fused)) return IBLB_OK;
+    if (c->transport == TR_LOCAL || (!slab && c->comm_stream) || (slab && env_long("IBLB_BAND_SLAB_OV", 1) == 0))
+        return IBLB_OK;
     if (!c->ncu) {
         hipDeviceProp_t prop;
         HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
