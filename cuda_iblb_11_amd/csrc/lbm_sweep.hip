@@ -559,9 +559,12 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
 
 // The walk over the level-1 columns.  (Unrolling it by two or three so that the window columns
 // are renamed instead of copied measured 10-20 % slower: more live registers, profiles/r02d_*.)
-template <typename T, int VS, int MODE, int K, bool SLAB, bool REV>
+// WL: the wave holds a wall row (compile-time, so that the waves of the other chunks carry no
+// wall code and keep no wall planes of the windows live)
+template <typename T, int VS, int MODE, int K, bool SLAB, bool REV, bool WL>
 __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
-                                              int lane, int r0, int et, bool owner, bool bot, bool top, bool walls) {
+                                              int lane, int r0, int et, bool owner, bool bot_, bool top_) {
+    const bool walls = WL, bot = WL && bot_, top = WL && top_;
     const int x0 = REV ? xb + K - 2 : xa - (K - 1);
     const int nl1 = xb - xa + 2 * (K - 1);  // level-1 columns xa-(K-1) .. xb+(K-2)
     T WA[K - 1][9][VS], WB[K - 1][9][VS];
@@ -635,10 +638,12 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     const bool top = et >= 0 && et < VS;
     // wave-uniform: does the wave hold a wall row (y = 0 or Y-1, ghost lanes included)?
     const bool walls = row0 <= 0 || row0 + 64 * VS >= a.L.ny;
+    const bool rev = a.alt && (sw & 1);
     const double q =
-        (a.alt && (sw & 1))
-            ? sweepk_walk<T, VS, MODE, K, SLAB, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top, walls)
-            : sweepk_walk<T, VS, MODE, K, SLAB, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top, walls);
+        walls ? (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
+                     : sweepk_walk<T, VS, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top))
+              : (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
+                     : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top));
     if (a.flux_col >= xa && a.flux_col < xb) {
         const double qs = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, qs);
