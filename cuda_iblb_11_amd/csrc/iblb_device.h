@@ -305,15 +305,20 @@ __device__ __forceinline__ void collide_sd(R f[9], const R s[4], const R d[4], R
         Qa[cl] = rho * b.oqa[cl];
         Rm[cl] = rho * b.omwi2[cl];
     }
+    // per pair: the even part A = hs s + E and the odd part B = hd d + O of the post-collision
+    // pair, f_a = A + B, f_b = A - B (7-8 fp64 operations per pair; the kernels are issue-bound
+    // on fp64, profiles/r02ai)
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         const int a = pair_a(p), bb = pair_b(p);
         const int cl = p < 2 ? 0 : 1;
-        const R cu = (R)cx(a) * ux + (R)cy(a) * uy;
-        const R E = fmaR(Qa[cl], cu * cu, fmaR(cu, k.hE[p], P[cl]));
+        const R cu = p == 0 ? ux : (p == 1 ? uy : (p == 2 ? ux + uy : uy - ux));  // c_a . u
+        const R E = fmaR(cu, fmaR(Qa[cl], cu, k.hE[p]), P[cl]);
         const R O = fmaR(Rm[cl], cu, k.gO[p]);
-        f[a] = fmaR(s[p], b.hs, fmaR(d[p], b.hd, E + O));
-        f[bb] = fmaR(s[p], b.hs, fmaR(d[p], b.nhd, E - O));
+        const R A = fmaR(s[p], b.hs, E);
+        const R B = fmaR(d[p], b.hd, O);
+        f[a] = A + B;
+        f[bb] = A - B;
     }
 }
 

@@ -1,714 +1,21 @@
-// lbm_sweep.hip — two reference iterations per launch (temporal blocking along x).
-//
-// The one-step collide-stream kernel (lbm_kernels.hip) already moves the algorithmic minimum of
-// one iteration, 144 B/LU in f64, at ~96 % of the measured HBM copy rate.  Below that floor the
-// only lever is to touch the state less often: this kernel reads g^t once and writes g^{t+2}
-// once, keeping the intermediate post-collision state g^{t+1} in registers.
-//
-// One wave = one (sweep, chunk): a chunk of 64*VS rows (lane l owns rows y0 .. y0+VS-1) and a
-// sweep of W output columns [xa, xb).  The wave walks x = xa-1 .. xb:
-//   step 1  g1[x]   = collide(pull(g0)) for its rows, plus ONE extra cell per lane: lane 0 the row
-//                     below the chunk (cs-1), lane 63 the row above (cs+64*VS).  Those are the
-//                     only g1 values of other chunks that step 2 pulls (c_y = +-1 planes).
-//   step 2  g2[x-1] = collide(pull(g1)) from the register window g1[x-2] (planes 1,5,8),
-//                     g1[x-1] (0,2,4 and the wall cells), g1[x] (3,6,7); +-1-row pulls are DPP
-//                     lane shifts whose end lanes take the extra cells.
-// Per cell and iteration the arithmetic is the one of fused_kernel (same relax_cell, same
-// storage rounding), so the result is bit-identical to two one-step launches.  Cost: the g1
-// columns xa-1 and xb are recomputed by the neighbouring sweeps and each lane collides VS+1
-// cells in step 1 (the extra cell is live in 2 lanes of 64).
-//
-// Algorithmic HBM bytes per launch: one read + one write of the state = 144 B per cell (f64) for
-// TWO lattice updates, plus the (W+2)/W re-read of the sweep edges.
-//
-// Single slab: columns -2, -1, ncol, ncol+1 are the periodic images.  Slab of a group: they come
-// from the 2-step halo (9 planes per side, slots in iblb_device.h: SWEEP_HALO_SLOTS), and the
-// kernel writes the 9 planes its neighbours need into the send buffers.
-#include "lbm_vec.h"
+// lbm_sweep.hip — two iterations per launch (sweep2_kernel), the dispatch of the K-iteration
+// sweeps (built per depth in lbm_sweepk<K>.hip) and the halo pack kernels; the kernels' code is
+// in lbm_sweep_impl.h.
+#include "lbm_sweep_impl.h"
 
 namespace iblb {
 
-enum { MODE_NO_PREFETCH = 8 };  // sweep only (MODE bits 1, 2 as in lbm_vec.h)
-
-namespace {
-
-// pointer to plane k of column x (x in [-2, ncol+1]); x is wave-uniform.  Computed, not looked
-// up: a table of halo pointers in the kernel arguments costs more SGPRs than a wave has.
-template <typename T, bool SLAB>
-__device__ __forceinline__ const T* sweep_col(const Sweep2Args<T>& a, int x, int k) {
-    const Layout& L = a.L;
-    if (x >= 0 && x < L.ncol) return a.src + (long)x * L.col + (long)k * L.plane;
-    if (!SLAB) {  // lone slab: periodic image
-        const int xw = x < 0 ? x + L.ncol : x - L.ncol;
-        return a.src + (long)xw * L.col + (long)k * L.plane;
-    }
-    if (x < 0) return a.recv_left + (long)sweep_slot(true, -1 - x, k) * L.rows;
-    return a.recv_right + (long)sweep_slot(false, x - L.ncol, k) * L.rows;
-}
-
-// g0(x, y, k) for the wall cells (y = 0 or Y-1) of column x; a group slab's halo columns carry
-// the same-cell values their walls need in slot 9
-template <typename T, bool SLAB>
-__device__ __forceinline__ T wall_val(const Sweep2Args<T>& a, int x, int k, int y) {
-    if (SLAB && x == -1 && (k == 7 || k == 6)) return a.recv_left[9 * a.L.rows + (y == 0 ? 0 : 1)];
-    if (SLAB && x == a.L.ncol && (k == 8 || k == 5)) return a.recv_right[9 * a.L.rows + (y == 0 ? 0 : 1)];
-    return sweep_col<T, SLAB>(a, x, k)[y];
-}
-
-// rows y0 .. y0+VS-1 of plane pointer p shifted by one row: DIR = +1 -> rows y-1, DIR = -1 ->
-// rows y+1, built from the aligned values v of this lane's rows; the end lane takes *edge (no
-// edge: the end lane keeps whatever the shift left, it is a ghost row whose value is not used)
-template <typename T, int VS, int DIR>
-__device__ __forceinline__ void shift_rows(const T v[VS], const T* edge, int lane, T r[VS]) {
-    if (DIR > 0) {
-        T prev = lane_shift<+1>(v[VS - 1]);
-        if (edge && lane == 0) prev = *edge;
-        r[0] = prev;
-#pragma unroll
-        for (int e = 1; e < VS; ++e) r[e] = v[e - 1];
-    } else {
-        T next = lane_shift<-1>(v[0]);
-        if (edge && lane == 63) next = *edge;
-#pragma unroll
-        for (int e = 0; e < VS - 1; ++e) r[e] = v[e + 1];
-        r[VS - 1] = next;
-    }
-}
-
-// Row-vector access at a wave-uniform base + this lane's 32-bit byte offset: the compiler keeps
-// the base in SGPRs (global_load/store saddr form) and every access shares one offset VGPR.
-// readfirstlane makes the base an opaque SGPR value, so the compiler cannot re-associate the
-// lane offset into a per-lane 64-bit address (2 VGPRs per access).
-template <typename P>
-__device__ __forceinline__ P* sgpr_ptr(P* p) {
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (P*)(((uint64_t)hi << 32) | lo);
-}
-#define IBLB_GLOBAL __attribute__((address_space(1)))
-
-template <typename T, int VS, int MODE>
-__device__ __forceinline__ void ld_rows(const T* base, unsigned off, T v[VS]) {
-    typedef typename VT<T, VS>::type vec;
-    const IBLB_GLOBAL vec* p = (const IBLB_GLOBAL vec*)((const IBLB_GLOBAL char*)sgpr_ptr(base) + off);
-    const vec x = (MODE & MODE_NT_LOAD) ? __builtin_nontemporal_load(p) : *p;
-#pragma unroll
-    for (int e = 0; e < VS; ++e) v[e] = x[e];
-}
-
-template <typename T, int VS, int MODE>
-__device__ __forceinline__ void st_rows(T* base, unsigned off, const T v[VS]) {
-    typedef typename VT<T, VS>::type vec;
-    vec x;
-#pragma unroll
-    for (int e = 0; e < VS; ++e) x[e] = v[e];
-    IBLB_GLOBAL vec* p = (IBLB_GLOBAL vec*)((IBLB_GLOBAL char*)sgpr_ptr(base) + off);
-    if (MODE & MODE_NT_STORE) __builtin_nontemporal_store(x, p);
-    else *p = x;
-}
-
-// Raw g0 rows of one column step: the 9 source planes at this lane's rows, plus the same-cell
-// values the walls need from planes whose pull column is not x (7, 8 at y = 0; 5, 6 at y = Y-1)
-template <typename T, int VS>
-struct Raw {
-    T v[9][VS];
-    T e[9];  // wave-edge rows: row0-1 of the c_y = +1 planes, row0+64*VS of the c_y = -1 planes
-    T w[4];  // g0(x, 0, 7), g0(x, 0, 8), g0(x, Y-1, 5), g0(x, Y-1, 6) (wall lanes only)
-};
-
-// rows of the wave start at row0 = cs - VS (uniform); lane byte offset off
-template <typename T, int VS, int MODE, bool SLAB>
-__device__ __forceinline__ void load_raw(const Sweep2Args<T>& a, int x, int row0, unsigned off, bool bot, bool top,
-                                         Raw<T, VS>& r) {
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        const T* p = sweep_col<T, SLAB>(a, x - cx(k), k) + row0;
-        ld_rows<T, VS, MODE>(p, off, r.v[k]);
-        // the ghost lanes' own pulls reach one row beyond the wave (uniform address)
-        if (cy(k) == 1) r.e[k] = p[-1];
-        if (cy(k) == -1) r.e[k] = p[64 * VS];
-    }
-    r.w[0] = r.w[1] = r.w[2] = r.w[3] = (T)0;
-    if (bot) {
-        r.w[0] = wall_val<T, SLAB>(a, x, 7, 0);
-        r.w[1] = wall_val<T, SLAB>(a, x, 8, 0);
-    }
-    if (top) {
-        r.w[2] = wall_val<T, SLAB>(a, x, 5, a.L.ny - 1);
-        r.w[3] = wall_val<T, SLAB>(a, x, 6, a.L.ny - 1);
-    }
-}
-
-// pull of the 9 populations of this lane's rows from one column triple of a post-collision
-// state held as aligned row vectors (pk[k]: plane k of column x - c_x(k)): planes with c_y = 0 as
-// they are, c_y = +1 from the row below (DPP shift up), c_y = -1 from the row above, the end
-// lanes taking edge[k] (the row beyond the wave; nullptr: garbage, see below); the walls
-// from the same cell of the middle column (planes 2, 4 of this lane's rows, 7 and 8 of row 0,
-// 5 and 6 of this lane's rows for the top row).  The end lanes' out-of-wave neighbours are garbage: those lanes are the
-// sweep's ghost rows.
-template <typename T, int VS>
-__device__ __forceinline__ void pull_window(const T (*pk[9])[VS], const T* edge, const T (&m2)[VS], const T (&m4)[VS],
-                                            T m7, T m8, const T (&m5)[VS], const T (&m6)[VS], int lane, int r0,
-                                            int et, T s[9][VS], bool walls = true) {
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        if (cy(k) == 0) {
-#pragma unroll
-            for (int e = 0; e < VS; ++e) s[k][e] = (*pk[k])[e];
-        } else if (cy(k) == 1) {
-            shift_rows<T, VS, +1>(*pk[k], edge ? edge + k : nullptr, lane, s[k]);
-        } else {
-            shift_rows<T, VS, -1>(*pk[k], edge ? edge + k : nullptr, lane, s[k]);
-        }
-    }
-    if (!walls) return;  // wave-uniform: the wave holds neither wall row
-    if (r0 == 0) {  // bounce-back on y = 0 (LatticeBoltzmann.cu:328-340)
-        s[2][0] = m4[0];
-        s[5][0] = m7;
-        s[6][0] = m8;
-    }
-    if (et >= 0 && et < VS) {  // same-cell mirror on y = Y-1 (LatticeBoltzmann.cu:341-353)
-#pragma unroll
-        for (int e = 0; e < VS; ++e)
-            if (e == et) { s[4][e] = m2[e]; s[8][e] = m5[e]; s[7][e] = m6[e]; }
-    }
-}
-
-}  // namespace
-
-// The walk of one wave over the output columns [xa, xb): step 1 makes g1 of columns xa-1 .. xb
-// in walking order, step 2 makes g2 of the middle column of the last three.  REV walks from xb
-// down to xa-1 (the window mirrored: A = g1[x+2], C = g1[x]); alternate sweeps walking towards
-// each other read their shared edge columns at the same time, so one fetch serves both.
-// Returns this lane's flux partial.
-template <typename T, int VS, int MODE, bool SLAB, bool REV>
-__device__ __forceinline__ double sweep_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
-                                             int lane, int r0, int et, bool owner, bool bot, bool top) {
-    typedef typename Calc<T>::R R;
-    constexpr bool DEV = Store<T>::dev;
-    const Layout L = a.L;
-    // first, last and next column of the walk
-    const int x0 = REV ? xb : xa - 1, x1 = REV ? xa - 1 : xb, dx = REV ? -1 : 1;
-
-    // g1 window: A = g1[x-2dx] (planes with c_x = dx used), B = g1[x-dx], C = g1[x]
-    T A[9][VS], B[9][VS];
-#pragma unroll
-    for (int k = 0; k < 9; ++k)
-#pragma unroll
-        for (int e = 0; e < VS; ++e) { A[k][e] = 0; B[k][e] = 0; }
-    double q = 0.;
-
-    // software prefetch of the next column (MODE_NO_PREFETCH: load at use, fewer VGPRs)
-    constexpr bool PF = !(MODE & MODE_NO_PREFETCH);
-    Raw<T, VS> nxt;
-    if (PF) load_raw<T, VS, MODE, SLAB>(a, x0, row0, off, bot, top, nxt);
-    for (int i = 0, x = x0; i <= xb - xa + 1; ++i, x += dx) {
-        Raw<T, VS> cur;
-        if (PF) {
-            cur = nxt;
-            load_raw<T, VS, MODE, SLAB>(a, x == x1 ? x : x + dx, row0, off, bot, top, nxt);
-        } else {
-            load_raw<T, VS, MODE, SLAB>(a, x, row0, off, bot, top, cur);
-        }
-
-        // ---- step 1: g1[x] ----
-        T C[9][VS];
-        {
-            const T(*pk[9])[VS];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) pk[k] = &cur.v[k];
-            T s[9][VS];
-            T t5[VS], t6[VS];
-#pragma unroll
-            for (int e = 0; e < VS; ++e) { t5[e] = cur.w[2]; t6[e] = cur.w[3]; }
-            pull_window<T, VS>(pk, cur.e, cur.v[2], cur.v[4], cur.w[0], cur.w[1], t5, t6, lane, r0, et, s);
-            const bool flux1 = x == a.flux_col && x >= xa && x < xb;
-#pragma unroll
-            for (int e = 0; e < VS; ++e) {
-                R f[9];
-#pragma unroll
-                for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
-                const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
-                if (flux1 && owner && r0 + e < L.ny) q += (double)ux / a.flux_norm;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) C[k][e] = (T)f[k];
-            }
-        }
-
-        // ---- step 2: g2[x-dx] from the window ----
-        if (i >= 2) {
-            const int xo = x - dx;
-            const T(*pk[9])[VS];
-            // plane k of g2[xo] pulls from g1[xo - c_x(k)]: c_x = dx -> A, c_x = -dx -> C
-#pragma unroll
-            for (int k = 0; k < 9; ++k) pk[k] = cx(k) == dx ? &A[k] : (cx(k) == -dx ? &C[k] : &B[k]);
-            T s[9][VS];
-            pull_window<T, VS>(pk, nullptr, B[2], B[4], B[7][0], B[8][0], B[5], B[6], lane, r0, et, s);
-            const bool flux2 = xo == a.flux_col;
-#pragma unroll
-            for (int e = 0; e < VS; ++e) {
-                R f[9];
-#pragma unroll
-                for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
-                const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
-                if (flux2 && owner && r0 + e < L.ny) q += (double)ux / a.flux_norm;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) s[k][e] = (T)f[k];
-            }
-            if (owner) {
-                T* dst = a.dst + (long)xo * L.col + row0;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * L.plane, off, s[k]);
-                if (SLAB) {  // the 2-step halo of g^{t+2} for the neighbours (iblb_kernels.h)
-                    const bool sl0 = xo == 0, sl1 = xo == 1, sr0 = xo == L.ncol - 1, sr1 = xo == L.ncol - 2;
-                    if (sl0 || sl1 || sr0 || sr1) {
-                        T* buf = (sl0 || sl1) ? a.send_left + row0 : a.send_right + row0;
-                        const bool left = sl0 || sl1;
-                        const int s0 = (sl0 || sr0) ? 0 : 6;
-                        const int ns = (sl0 || sr0) ? 6 : 3;
-#pragma unroll
-                        for (int q = 0; q < 6; ++q) {
-                            if (q >= ns) break;
-                            const int sl = s0 + q;
-                            // slot sl carries plane sweep_send_plane(left, sl)
-                            T v[VS];
-#pragma unroll
-                            for (int k = 0; k < 9; ++k)
-                                if (k == (left ? sweep_send_plane(true, sl) : sweep_send_plane(false, sl)))
-#pragma unroll
-                                    for (int e = 0; e < VS; ++e) v[e] = s[k][e];
-                            st_rows<T, VS, 0>(buf + (long)sl * L.rows, off, v);
-                        }
-                        if (sl0 || sr0) {  // slot 9: the same-cell wall values of this column
-                            T* w = buf - row0 + 9 * L.rows;
-                            if (bot) w[0] = sl0 ? s[8][0] : s[7][0];
-#pragma unroll
-                            for (int e = 0; e < VS; ++e)
-                                if (top && e == et) w[1] = sl0 ? s[5][e] : s[6][e];
-                        }
-                    }
-                }
-            }
-        }
-
-        // ---- rotate the window ----
-#pragma unroll
-        for (int k = 0; k < 9; ++k)
-#pragma unroll
-            for (int e = 0; e < VS; ++e) { A[k][e] = B[k][e]; B[k][e] = C[k][e]; }
-    }
-    return q;
-}
-
-// One wave = (sweep, chunk).  Lane l holds rows r0 = cs - VS + l*VS .. r0+VS-1: lanes 1..62 own
-// the chunk's 62*VS output rows [cs, cs + 62*VS), lanes 0 and 63 are ghost rows (the g1 values
-// of the rows just outside the chunk that step 2 pulls).  Ghost rows and rows >= ny compute
-// garbage that no owned row reads.
-template <typename T, int VS, int MODE, bool SLAB>
-__global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
-    typedef typename Calc<T>::R R;
-    static_assert(sizeof(R) == sizeof(T), "the window keeps g1 in the storage type");
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int sw, ch;
-    if (a.map == 0) {
-        // a workgroup = 4 neighbouring sweeps of one chunk (their shared edge columns are read
-        // once from HBM), workgroups remapped so that each XCD (blocks b = 8*slot + xcd) walks a
-        // contiguous range of (chunk, sweep group): neighbouring groups run on one L2
-        const int nb = (int)gridDim.x, b = (int)blockIdx.x, q = nb / 8;
-        const int work = b < 8 * q ? (b % 8) * q + b / 8 : b;
-        const int ngroups = (a.nsweep + 3) / 4;
-        ch = work / ngroups;
-        sw = (work - ch * ngroups) * 4 + wv;
-    } else {
-        // linear: wave -> (sweep, chunk), chunk fastest.  map 2: the same order dealt to the
-        // XCDs in contiguous ranges (blocks b and b+8 share an XCD), so the edge columns of
-        // neighbouring sweeps are re-read from the L2 that just fetched them
-        int b = (int)blockIdx.x;
-        if (a.map == 2) {
-            const int q = (int)gridDim.x / 8;
-            if (b < 8 * q) b = (b % 8) * q + b / 8;
-        }
-        const int gw = b * 4 + wv;
-        sw = gw / a.nch;
-        ch = gw - sw * a.nch;
-    }
-    if (sw >= a.nsweep || ch >= a.nch) return;
-    const int xa = a.col_begin + sw * a.col_step;
-    const int xb = min(xa + a.W, a.col_end);
-    const int cs = ch * (62 * VS);
-    const int row0 = cs - VS;  // first row of the wave (lane 0)
-    const int r0 = row0 + lane * VS;
-    const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
-    const int et = a.L.ny - 1 - r0;  // element of the top row, if in [0, VS)
-    const bool owner = lane >= 1 && lane <= 62 && r0 < a.L.ny;
-    const bool bot = r0 == 0;
-    const bool top = et >= 0 && et < VS;
-    const double q = (a.alt && (sw & 1))
-                         ? sweep_walk<T, VS, MODE, SLAB, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
-                         : sweep_walk<T, VS, MODE, SLAB, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top);
-    if (a.flux_col >= xa && a.flux_col < xb) {
-        const double qs = wave_sum(q);
-        if (lane == 0) atomicAdd(a.Q, qs);
-    }
-}
-
-template <typename T, int VS, int MODE>
-static hipError_t launch_sweep_mode(const Sweep2Args<T>& a, bool slab, unsigned blocks, hipStream_t s) {
-    if (slab) sweep2_kernel<T, VS, MODE, true><<<blocks, 256, 0, s>>>(a);
-    else sweep2_kernel<T, VS, MODE, false><<<blocks, 256, 0, s>>>(a);
-    return hipGetLastError();
-}
-
-template <typename T, int VS>
-static hipError_t launch_sweep_vs(const Sweep2Args<T>& a, bool slab, unsigned blocks, hipStream_t s) {
-    switch (a.variant) {
-        case 1: return launch_sweep_mode<T, VS, 1>(a, slab, blocks, s);
-        case 2: return launch_sweep_mode<T, VS, 2>(a, slab, blocks, s);
-        case 3: return launch_sweep_mode<T, VS, 3>(a, slab, blocks, s);
-        case 8: return launch_sweep_mode<T, VS, 8>(a, slab, blocks, s);
-        case 9: return launch_sweep_mode<T, VS, 9>(a, slab, blocks, s);
-        default: return launch_sweep_mode<T, VS, 0>(a, slab, blocks, s);
-    }
-}
-
-template <typename T>
-hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s) {
-    if (a.nsweep <= 0) return hipSuccess;
-    // rows are read up to VS+1 below 0 and up to nch*62*VS + VS (< rows + 62*VS + VS + 1): inside
-    // the 512-element guards of the buffers (iblb_ctx.hip)
-    if (a.W <= 0 || a.L.ncol < 2 || a.vs <= 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 || a.L.col % a.vs != 0)
-        return hipErrorInvalidValue;
-    if (slab && (!a.recv_left || !a.recv_right || !a.send_left || !a.send_right)) return hipErrorInvalidValue;
-    a.nch = (a.L.ny + 62 * a.vs - 1) / (62 * a.vs);
-    const unsigned blocks = a.map == 0 ? (unsigned)(((a.nsweep + 3) / 4) * (long)a.nch)
-                                       : (unsigned)(((long)a.nsweep * a.nch + 3) / 4);
-    constexpr int V = vec_of<T>();
-    if (a.vs == V) return launch_sweep_vs<T, V>(a, slab, blocks, s);
-    if (a.vs == V / 2) return launch_sweep_vs<T, V / 2>(a, slab, blocks, s);
-    return hipErrorInvalidValue;
-}
-
-// ---- K iterations per launch (lone slab, K = 3 .. 6) ------------------------------------------
-// sweepk_kernel: g^t -> g^{t+K}, the walk keeping K-1 register windows (g^{t+1} .. g^{t+K-1}).
-// Same wave geometry, order and walking directions as sweep2_kernel.  Valid rows shrink by one
-// per level at the wave's edges (the +-1-row pulls of the end lanes take garbage from level 2
-// on), so each edge carries G ghost lanes with G * VS >= K - 1 rows.  Each level's cell
-// arithmetic is fused_kernel's (relax_cell): bit-identical to K one-step launches.
-//
-// Software-pipelined walk over the level-1 columns xa-(K-1) .. xb+(K-2) (dx = +1, or -1 from
-// the right end): iteration i makes level 1 of column x from the rows loaded in the previous
-// iteration, issues the loads of column x + dx, then makes level l = 2 .. K of column
-// x - (l-1)*dx from level l-1's window.  The loads fly while K-1 levels of arithmetic run, and
-// every level (level 1 included) keeps only its two previous columns between iterations.
-// Wall rows (y = 0, Y-1) are patched only by the waves that hold them (a wave-uniform branch).
-//
-// Algorithmic HBM bytes per launch: one read + one write of the state (144 B per cell in f64)
-// for K lattice updates, plus the edge re-reads of neighbouring sweeps (served by L2 under the
-// XCD-contiguous alternating order).
-
-// plane k of column x of a lone slab, x periodic (x may lie up to K columns outside)
-template <typename T>
-__device__ __forceinline__ const T* col_periodic(const Sweep2Args<T>& a, int x, int k) {
-    const int n = a.L.ncol;
-    int xw = x % n;
-    if (xw < 0) xw += n;
-    return a.src + (long)xw * a.L.col + (long)k * a.L.plane;
-}
-
-// plane k of column x for the deep walk: a lone slab wraps periodically; a slab of a group
-// (SLAB) reads columns beyond its edges from the deep halo (deep_slot, K columns per side)
-template <typename T, bool SLAB, int K>
-__device__ __forceinline__ const T* col_deep(const Sweep2Args<T>& a, int x, int k) {
-    if (!SLAB) return col_periodic<T>(a, x, k);
-    if (x < 0) return a.recv_left + (long)deep_slot(true, -1 - x, k, K) * a.L.rows;
-    if (x >= a.L.ncol) return a.recv_right + (long)deep_slot(false, x - a.L.ncol, k, K) * a.L.rows;
-    return a.src + (long)x * a.L.col + (long)k * a.L.plane;
-}
-
-template <typename T, int VS, int MODE, bool SLAB, int K>
-__device__ __forceinline__ void load_raw_periodic(const Sweep2Args<T>& a, int x, int row0, unsigned off, bool bot,
-                                                  bool top, Raw<T, VS>& r) {
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        const T* p = col_deep<T, SLAB, K>(a, x - cx(k), k) + row0;
-        ld_rows<T, VS, MODE>(p, off, r.v[k]);
-        if (cy(k) == 1) r.e[k] = p[-1];
-        if (cy(k) == -1) r.e[k] = p[64 * VS];
-    }
-    r.w[0] = r.w[1] = r.w[2] = r.w[3] = (T)0;
-    if (bot) {
-        r.w[0] = col_deep<T, SLAB, K>(a, x, 7)[0];
-        r.w[1] = col_deep<T, SLAB, K>(a, x, 8)[0];
-    }
-    if (top) {
-        r.w[2] = col_deep<T, SLAB, K>(a, x, 5)[a.L.ny - 1];
-        r.w[3] = col_deep<T, SLAB, K>(a, x, 6)[a.L.ny - 1];
-    }
-}
-
-// one column of level l+1 from a window of level l (A = older, B = middle, C = newer column in
-// walking direction DX): the output is B's column; flux: add u_x of the owned rows to q
-template <typename T, int VS, int DX>
-__device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (&B)[9][VS], const T (&C)[9][VS],
-                                                  const Sweep2Args<T>& a, int lane, int r0, int et, bool walls,
-                                                  bool flux, bool owner, double& q, T (&out)[9][VS]) {
-    typedef typename Calc<T>::R R;
-    constexpr bool DEV = Store<T>::dev;
-    const T(*pk[9])[VS];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) pk[k] = cx(k) == DX ? &A[k] : (cx(k) == -DX ? &C[k] : &B[k]);
-    T s[9][VS];
-    pull_window<T, VS>(pk, nullptr, B[2], B[4], B[7][0], B[8][0], B[5], B[6], lane, r0, et, s, walls);
-#pragma unroll
-    for (int e = 0; e < VS; ++e) {
-        R f[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
-        const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
-        if (flux && owner && r0 + e < a.L.ny) q += (double)ux / a.flux_norm;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) out[k][e] = (T)f[k];
-    }
-}
-
-// level 1 of one column from its loaded g^t rows
-template <typename T, int VS>
-__device__ __forceinline__ void level_from_raw(const Raw<T, VS>& cur, const Sweep2Args<T>& a, int lane, int r0, int et,
-                                               bool walls, bool flux, bool owner, double& q, T (&out)[9][VS]) {
-    typedef typename Calc<T>::R R;
-    constexpr bool DEV = Store<T>::dev;
-    const T(*pk[9])[VS];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) pk[k] = &cur.v[k];
-    T s[9][VS];
-    T t5[VS], t6[VS];
-#pragma unroll
-    for (int e = 0; e < VS; ++e) { t5[e] = cur.w[2]; t6[e] = cur.w[3]; }
-    pull_window<T, VS>(pk, cur.e, cur.v[2], cur.v[4], cur.w[0], cur.w[1], t5, t6, lane, r0, et, s, walls);
-#pragma unroll
-    for (int e = 0; e < VS; ++e) {
-        R f[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
-        const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
-        if (flux && owner && r0 + e < a.L.ny) q += (double)ux / a.flux_norm;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) out[k][e] = (T)f[k];
-    }
-}
-
-template <typename T, int VS>
-__device__ __forceinline__ void copy_col(T (&d)[9][VS], const T (&s)[9][VS]) {
-#pragma unroll
-    for (int k = 0; k < 9; ++k)
-#pragma unroll
-        for (int e = 0; e < VS; ++e) d[k][e] = s[k][e];
-}
-
-// Iteration i of the walk (column x = x0 + i*dx): level 1 of x from the rows loaded in the
-// previous iteration, then the loads of column x + dx (they fly during the remaining levels),
-// then level l = 2 .. K of column x - (l-1)*dx from level l-1's window: WA / WB = its columns
-// made two and one iterations ago, and N = the one made in this iteration.  Level l starts at
-// iteration 2(l-1), when its window holds three valid columns; its columns in [xa, xb) (stored at
-// level K, counted in the flux) all come later.  (Running every level from iteration 0 instead,
-// on not-yet-valid windows, lets the compiler hoist the collide constants out of the walk and
-// needs more registers than the wave has: measured 40 % slower, profiles/r02c_*.)
-template <typename T, int VS, int MODE, int K, bool SLAB, bool REV>
-__device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int nl1, int x0, int xa, int xb, int row0,
-                                            unsigned off, int lane, int r0, int et, bool owner, bool bot, bool top,
-                                            bool walls, T (&WA)[K - 1][9][VS], T (&WB)[K - 1][9][VS],
-                                            Raw<T, VS>& cur, double& q) {
-    constexpr int DX = REV ? -1 : 1;
-    const int x = x0 + i * DX;
-    T N[9][VS];
-    level_from_raw<T, VS>(cur, a, lane, r0, et, walls, x == a.flux_col && x >= xa && x < xb, owner, q, N);
-    if (i + 1 < nl1) load_raw_periodic<T, VS, MODE, SLAB, K>(a, x + DX, row0, off, bot, top, cur);
-#pragma unroll
-    for (int l = 2; l <= K; ++l) {
-        const int c = x - (l - 1) * DX;
-        const bool mine = c >= xa && c < xb;  // implies made (see above)
-        const bool flux = mine && c == a.flux_col;
-        T out[9][VS];
-        const bool made = i >= 2 * (l - 1);
-        if (made) level_from_window<T, VS, DX>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, owner, q, out);
-        if (made && l == K && mine && owner) {
-            T* dst = a.dst + (long)c * a.L.col + row0;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * a.L.plane, off, out[k]);
-            // slab of a group: the output columns within K of an edge are the deep halo the
-            // neighbour needs next cycle (wave-uniform: c is the walk's column); written here
-            // instead of by a pack kernel after the sweep
-            if (SLAB && a.send_left && (c < K || c >= a.L.ncol - K)) {
-                const bool to_left = c < K;
-                const int d = to_left ? c : a.L.ncol - 1 - c;
-                T* sb = (to_left ? a.send_left : a.send_right) + row0;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    const int slot = deep_slot(!to_left, d, k, K);
-                    if (slot >= 0) st_rows<T, VS, 0>(sb + (long)slot * a.L.rows, off, out[k]);
-                }
-            }
-        }
-        copy_col<T, VS>(WA[l - 2], WB[l - 2]);
-        copy_col<T, VS>(WB[l - 2], N);
-        if (l < K && made) copy_col<T, VS>(N, out);
-    }
-}
-
-// The walk over the level-1 columns.  (Unrolling it by two or three so that the window columns
-// are renamed instead of copied measured 10-20 % slower: more live registers, profiles/r02d_*.)
-// WL: the wave holds a wall row (compile-time, so that the waves of the other chunks carry no
-// wall code and keep no wall planes of the windows live)
-template <typename T, int VS, int MODE, int K, bool SLAB, bool REV, bool WL>
-__device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
-                                              int lane, int r0, int et, bool owner, bool bot_, bool top_) {
-    const bool walls = WL, bot = WL && bot_, top = WL && top_;
-    const int x0 = REV ? xb + K - 2 : xa - (K - 1);
-    const int nl1 = xb - xa + 2 * (K - 1);  // level-1 columns xa-(K-1) .. xb+(K-2)
-    T WA[K - 1][9][VS], WB[K - 1][9][VS];
-#pragma unroll
-    for (int l = 0; l < K - 1; ++l)
-#pragma unroll
-        for (int k = 0; k < 9; ++k)
-#pragma unroll
-            for (int e = 0; e < VS; ++e) WA[l][k][e] = WB[l][k][e] = (T)0;
-    double q = 0.;
-    Raw<T, VS> cur;
-    load_raw_periodic<T, VS, MODE, SLAB, K>(a, x0, row0, off, bot, top, cur);
-    for (int i = 0; i < nl1; ++i)
-        sweepk_iter<T, VS, MODE, K, SLAB, REV>(a, i, nl1, x0, xa, xb, row0, off, lane, r0, et, owner, bot, top, walls, WA,
-                                               WB, cur, q);
-    return q;
-}
-
-// wave -> (sweep, chunk) of the linear order, optionally dealt to the XCDs in contiguous ranges
-// (xcds: the XCDs the launch's workgroups are dealt over, 0 = 8; the dispatcher deals over all
-// eight whatever the stream's CU mask, profiles/r02n_xcc_probe.txt)
-__device__ __forceinline__ void linear_item(int map, int nch, int xcds, int wv, int& sw, int& ch) {
-    int b = (int)blockIdx.x;
-    if (map == 2) {
-        const int nx = xcds > 0 ? xcds : 8;
-        const int q = (int)gridDim.x / nx;
-        if (b < nx * q) b = (b % nx) * q + b / nx;
-    }
-    const int gw = b * 4 + wv;
-    sw = gw / nch;
-    ch = gw - sw * nch;
-}
-
-template <int K, int VS>
-constexpr int ghost_lanes() { return (K - 1 + VS - 1) / VS; }
-
-// G ghost lanes at each wave edge (G * VS >= K - 1 rows)
-template <typename T, int VS, int MODE, int K, bool SLAB>
-__global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
-    constexpr int G = ghost_lanes<K, VS>();
-    constexpr int OWN = 64 - 2 * G;  // owned lanes per wave
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int sw, ch;
-    linear_item(a.map, a.nch, a.xcds, wv, sw, ch);
-    if (sw >= a.nsweep || ch >= a.nch) return;
-    int xa, xb;
-    if (a.sweep_tab && a.tab_rows) {
-        const int* e = a.sweep_tab + 4 * sw;
-        if (ch < e[2] || ch >= e[3]) return;  // wave-uniform: rows of an IB patch
-        xa = __builtin_amdgcn_readfirstlane(e[0]);
-        xb = __builtin_amdgcn_readfirstlane(e[1]);
-    } else if (a.sweep_tab) {
-        xa = __builtin_amdgcn_readfirstlane(a.sweep_tab[2 * sw]);
-        xb = __builtin_amdgcn_readfirstlane(a.sweep_tab[2 * sw + 1]);
-    } else if (a.col_step > 0) {
-        xa = a.col_begin + sw * a.col_step;
-        xb = min(xa + a.W, a.col_end);
-    } else {  // balanced: nsweep sweeps of floor/ceil((col_end - col_begin) / nsweep) columns
-        const long n = a.col_end - a.col_begin;
-        xa = a.col_begin + (int)(sw * n / a.nsweep);
-        xb = a.col_begin + (int)((sw + 1) * n / a.nsweep);
-    }
-    const int cs = ch * (OWN * VS);
-    const int row0 = cs - G * VS;
-    const int r0 = row0 + lane * VS;
-    const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
-    const int et = a.L.ny - 1 - r0;
-    const bool owner = lane >= G && lane < 64 - G && r0 < a.L.ny;
-    const bool bot = r0 == 0;
-    const bool top = et >= 0 && et < VS;
-    // wave-uniform: does the wave hold a wall row (y = 0 or Y-1, ghost lanes included)?
-    const bool walls = row0 <= 0 || row0 + 64 * VS >= a.L.ny;
-    const bool rev = a.alt && (sw & 1);
-    const double q =
-        walls ? (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
-                     : sweepk_walk<T, VS, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top))
-              : (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
-                     : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top));
-    if (a.flux_col >= xa && a.flux_col < xb) {
-        const double qs = wave_sum(q);
-        if (lane == 0) atomicAdd(a.Q, qs);
-    }
-}
-
-// Waves of one instantiation resident per CU (256-thread workgroups), and on `cus` CUs (0: all).
-template <typename T, int VS, int MODE, int K, bool SLAB>
-static long waves_per_cu() {
-    static long cached = 0;
-    if (cached) return cached;
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweepk_kernel<T, VS, MODE, K, SLAB>, 256, 0) != hipSuccess ||
-        nb <= 0)
-        return 0;
-    cached = (long)nb * 4;
-    return cached;
-}
-template <typename T, int VS, int MODE, int K, bool SLAB>
-static long resident_waves(int cus) {
-    int dev = 0, ncu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-        return 0;
-    return waves_per_cu<T, VS, MODE, K, SLAB>() * (cus > 0 ? std::min(cus, ncu) : ncu);
-}
-
-template <typename T, int VS, int MODE, int K, bool SLAB>
-static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s) {
-    if (b.col_step <= 0 && !b.sweep_tab) {
-        // balanced sweeps: the wave count a whole number of device-wide rounds (the waves of one
-        // launch all do the same work, so a partial last round idles the chip), sweeps close to
-        // the requested W columns
-        const long n = b.col_end - b.col_begin;
-        const long slots = resident_waves<T, VS, MODE, K, SLAB>(b.cus);
-        long ns = (n + b.W - 1) / b.W;
-        if (slots > 0) {
-            const long rounds = std::max(1L, (ns * b.nch + slots / 2) / slots);
-            ns = std::max(1L, rounds * slots / b.nch);
-        }
-        b.nsweep = (int)std::min(ns, n);
-    }
-    const unsigned blocks = (unsigned)(((long)b.nsweep * b.nch + 3) / 4);
-    sweepk_kernel<T, VS, MODE, K, SLAB><<<blocks, 256, 0, s>>>(b);
-    return hipGetLastError();
-}
-
-template <typename T, int VS, int K, bool SLAB>
-static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s) {
-    constexpr int G = ghost_lanes<K, VS>();
-    const int rows_per_wave = (64 - 2 * G) * VS;  // owned rows
-    Sweep2Args<T> b = a;
-    b.nch = (a.L.ny + rows_per_wave - 1) / rows_per_wave;
-    // variants: 1 = nontemporal stores (default), 0 = plain
-    if (a.variant == 0) return launch_sweepk_mode<T, VS, 0, K, SLAB>(b, s);
-    return launch_sweepk_mode<T, VS, 1, K, SLAB>(b, s);
-}
-
-// cells per lane: 2 or 1 (4 in f32 measured slower: one wave per SIMD, profiles/r01d4_*)
-template <typename T, int K, bool SLAB>
-static hipError_t launch_sweepk_depth(const Sweep2Args<T>& a, hipStream_t s) {
-    if (a.vs == 2) return launch_sweepk_vs<T, 2, K, SLAB>(a, s);
-    if (a.vs == 1) return launch_sweepk_vs<T, 1, K, SLAB>(a, s);
-    return hipErrorInvalidValue;
-}
+// the K-iteration kernels are built in lbm_sweepk<K>.hip
+#define IBLB_SWEEPK_EXTERN(T, K, S)                                                          \
+    extern template hipError_t launch_sweepk_depth<T, K, S>(const Sweep2Args<T>&, hipStream_t); \
+    extern template int deep_geometry<T, K, S>(int, int, int, int*);
+#define IBLB_SWEEPK_EXTERN_K(K)                                                                               \
+    IBLB_SWEEPK_EXTERN(double, K, false) IBLB_SWEEPK_EXTERN(double, K, true) IBLB_SWEEPK_EXTERN(float, K, false) \
+    IBLB_SWEEPK_EXTERN(float, K, true)
+IBLB_SWEEPK_EXTERN_K(3)
+IBLB_SWEEPK_EXTERN_K(4)
+IBLB_SWEEPK_EXTERN_K(5)
+IBLB_SWEEPK_EXTERN_K(6)
 
 template <typename T, bool SLAB>
 static hipError_t launch_sweepk_slab(const Sweep2Args<T>& a, int depth, hipStream_t s) {
@@ -719,17 +26,6 @@ static hipError_t launch_sweepk_slab(const Sweep2Args<T>& a, int depth, hipStrea
     return hipErrorInvalidValue;
 }
 
-// resident waves per CU and waves per launch column-chunk geometry of one configuration (the
-// context sizes the CUs it reserves for the boundary sweeps with it)
-template <typename T, int K, bool SLAB>
-static int deep_geometry(int vs, int variant, int ny, int* nch) {
-    if (vs == 2) {
-        *nch = (ny + (64 - 2 * ghost_lanes<K, 2>()) * 2 - 1) / ((64 - 2 * ghost_lanes<K, 2>()) * 2);
-        return (int)(variant == 0 ? waves_per_cu<T, 2, 0, K, SLAB>() : waves_per_cu<T, 2, 1, K, SLAB>());
-    }
-    *nch = (ny + (64 - 2 * ghost_lanes<K, 1>()) - 1) / (64 - 2 * ghost_lanes<K, 1>());
-    return (int)(variant == 0 ? waves_per_cu<T, 1, 0, K, SLAB>() : waves_per_cu<T, 1, 1, K, SLAB>());
-}
 
 template <typename T>
 int sweepk_geometry(int depth, int vs, int variant, bool slab, int ny, int* nch) {
