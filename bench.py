@@ -422,9 +422,9 @@ def main():
                 "unit": "GB/s",
                 "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": (f"sweepk_kernel<K={iters_per_launch}> (lbm_sweep.hip): {iters_per_launch} iterations per "
+                "kernel": (f"sweepk_kernel<K={iters_per_launch}> (lbm_sweep_impl.h): {iters_per_launch} iterations per "
                            "launch, state read and written once" if iters_per_launch > 2 else
-                           "sweep2_kernel (lbm_sweep.hip): two iterations per launch, state read and written once"
+                           "sweep2_kernel (lbm_sweep_impl.h): two iterations per launch, state read and written once"
                            if sweep else "fused_kernel (lbm_kernels.hip)"),
                 "bytes_per_cell": bytes_per_cell,
                 "cells_per_launch": cells_per_launch,
