@@ -230,6 +230,7 @@ struct KBase {
     R kw[2], kwi4[2], kwi2[2];  // k w, k w / cs^4, k w / cs^2   (k = 1 - 1/(2 TAU))
     R a1, ics2;            // 1/(2 cs^2), 1/cs^2
     R hs, hd, nhd;         // (1-w+)/2, (1-w-)/2, -(1-w-)/2
+    R nck[2];              // -k w / cs^2 (the forcing's even part per weight class: u.F times it)
 };
 // Force-dependent constants (uniform for a body force; per cell with an IB force)
 template <typename R>
@@ -254,6 +255,7 @@ __host__ __device__ inline KBase<R> make_kbase(const Coef& c) {
         b.kw[cl] = kk * w;
         b.kwi4[cl] = b.kw[cl] * ics4;
         b.kwi2[cl] = b.kw[cl] * ics2;
+        b.nck[cl] = -(ics2 * b.kw[cl]);
     }
     b.a1 = (R)c.inv_2cs2;
     b.ics2 = ics2;
@@ -289,19 +291,16 @@ __device__ __forceinline__ void collide_sd(R f[9], const R s[4], const R d[4], R
     const R usq = ux * ux + uy * uy;
     const R uF = ux * k.Fx + uy * k.Fy;
     const R base = -usq * b.a1;            // even equilibrium part common to all i
-    const R ebase = DEV ? base : (R)1 + base;
-    const R guF = -uF * b.ics2;
+    // rho (1 + base), the even equilibrium factor (deviation form: minus the rest density 1)
+    const R rb = DEV ? fmaR(rho, base, sum) : rho * ((R)1 + base);
     // rest population: f0 - w+ (f0 - feq0) = (1 - w+) f0 + w+ feq0
-    {
-        const R feq0w = DEV ? fmaR(rho, base, sum) * b.opw0 : (rho * ebase) * b.opw0;
-        f[0] = fmaR(b.omp, f[0], feq0w);
-    }
-    // per weight class: E = P + Qa cu^2 + cu hE_p,  O = Rm cu + gO_p
+    f[0] = fmaR(b.omp, f[0], rb * b.opw0);
+    // per weight class: E = P + Qa cu^2 + cu hE_p,  O = Rm cu + gO_p, with
+    // P = w+ w rho (1 + base) - k w (u.F) / cs^2
     R P[2], Qa[2], Rm[2];
 #pragma unroll
     for (int cl = 0; cl < 2; ++cl) {
-        P[cl] = fmaR(rho * b.opw[cl], ebase, guF * b.kw[cl]);
-        if (DEV) P[cl] = fmaR(sum, b.opw[cl], P[cl]);
+        P[cl] = fmaR(rb, b.opw[cl], uF * b.nck[cl]);
         Qa[cl] = rho * b.oqa[cl];
         Rm[cl] = rho * b.omwi2[cl];
     }
