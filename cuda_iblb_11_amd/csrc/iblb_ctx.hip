@@ -138,6 +138,11 @@ struct iblb_ctx {
     // IB included; IBLB_BAND_FUSED=1) instead of 2K dependent launches (default: one workgroup
     // per patch is latency-bound, K3 0.25 vs 0.09 ms per cycle, profiles/r02ad)
     int band_fused = 0;
+    // the cycle's deep sweep over every column (IBLB_BAND_FULL, default) instead of the table of
+    // gaps and band columns outside the patch rows: the patch rows it gets wrong (no force) are
+    // overwritten by the trapezoid's last level, which waits for it (ev_bd)
+    int band_full = 1;
+    hipEvent_t ev_bd = nullptr;
     int band_npatch = 0, band_pt_off = 0;  // patches; their table in d_band (BAND_PT ints each)
     char* s_alloc = nullptr;             // two scratch population buffers of the trapezoid
     void* sbuf[2] = {nullptr, nullptr};
@@ -769,6 +774,7 @@ bool band_ready(const iblb_ctx* c) {
            !c->cilia_on && ib_active(c) && c->sweep_on && c->sweep_depth >= 3;
 }
 
+bool band_full_deep(const iblb_ctx* c);
 template <typename T>
 int band_deep(iblb_ctx* c, int K, hipStream_t ds);
 template <typename T>
@@ -893,8 +899,33 @@ int band_step(iblb_ctx* c) {
 
 // the deep sweep of a band cycle over the force-free gaps (and the band columns outside the
 // patch rows): the sweep table of the plan
+// the full-lattice deep sweep of a band cycle (band_full): every column of a lone slab, the
+// interior [K, ncol-K) of a group slab; flux column in a band output: the table (the full sweep
+// would add the patch rows' force-free flux)
+bool band_full_deep(const iblb_ctx* c) { return c->band_full && !c->band_fused && c->band_flux < 0; }
+
 template <typename T>
 int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
+    if (band_full_deep(c)) {
+        const bool slab = !single_slab(c);
+        const int lo = slab ? K : 0, hi = slab ? c->ncol - K : c->ncol, n = hi - lo;
+        if (n <= 0) return IBLB_OK;
+        const int W = std::max(1, c->deep_w);
+        Sweep2Args<T> d = sweep_args<T>(c, lo, c->deep_balance ? 0 : W, hi, (n + W - 1) / W, W);
+        d.vs = c->deep_vs;
+        d.variant = c->deep_variant;
+        if (d.map == 0) d.map = 2;
+        d.cus = (slab ? c->ncu - c->reserved_cus : c->ncu) - c->band_reserve;  // the deep stream's CUs
+        if (!c->ncu) d.cus = 0;
+        d.xcds = (int)env_long("IBLB_DEEP_XCDS", 0);
+        size_t ev = 0;
+        int rc = ev_begin(c, &ev, ds);
+        if (rc) return rc;
+        HIP_TRY(c, launch_sweepk<T>(d, K, false, ds));
+        if ((rc = ev_end(c, ev, EV_SWEEPK, (long long)n * c->ny, ds))) return rc;
+        if (c->band_st) HIP_TRY(c, hipEventRecord(c->ev_bd, ds));
+        return IBLB_OK;
+    }
     if (c->band_nsweep <= 0) return IBLB_OK;
     Sweep2Args<T> d = sweep_args<T>(c, 0, 1, c->ncol, c->band_nsweep, std::max(1, c->deep_w));
     d.sweep_tab = c->d_band + c->band_sweep_off;
@@ -975,6 +1006,9 @@ int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool slab, h
         a.c = c->coef;
         a.k = c->kc;
         a.variant = c->variant;
+        // full deep sweep: it wrote (force-free) values into the patch rows of g^{t+K} too; the
+        // last level overwrites them after it
+        if (j == K - 1 && band_full_deep(c) && bs != ds) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_bd, 0));
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, bs))) return rc;
         HIP_TRY(c, launch_fused<T>(a, bs));
@@ -1325,6 +1359,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     }
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_fused = (int)env_long("IBLB_BAND_FUSED", 0);
+    c->band_full = (int)env_long("IBLB_BAND_FULL", 1);
     // halo buffers: recv_left, recv_right, send_left, send_right; each 10 (2-step) or 21 (IB)
     // slots + guards
     {
@@ -1366,7 +1401,7 @@ void iblb_destroy(iblb_ctx* c) {
             (void)hipStreamSynchronize(st);
             (void)hipStreamDestroy(st);
         }
-    for (hipEvent_t e : {c->ev_b0, c->ev_b1, c->ev_b2})
+    for (hipEvent_t e : {c->ev_b0, c->ev_b1, c->ev_b2, c->ev_bd})
         if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < 4; ++i) {
         if (c->band_pin_ev[i]) (void)hipEventDestroy(c->band_pin_ev[i]);
@@ -1514,7 +1549,7 @@ static int band_streams(iblb_ctx* c, long long band_lu, long long deep_lu, int n
         }
         HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->deep_st, (uint32_t)deep.size(), deep.data()));
         HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->band_st, (uint32_t)band.size(), band.data()));
-        for (hipEvent_t* e : {&c->ev_b0, &c->ev_b1, &c->ev_b2})
+        for (hipEvent_t* e : {&c->ev_b0, &c->ev_b1, &c->ev_b2, &c->ev_bd})
             if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventDisableSystemFence));
     }
     c->band_reserve = (int)want;
