@@ -615,11 +615,12 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
                                             unsigned off, int lane, int r0, int et, bool owner, bool bot, bool top,
                                             bool walls, T (&WA)[K - 1][9][VS], T (&WB)[K - 1][9][VS],
                                             Raw<T, VS>& cur, double& q, const BufOfs& bo,
-                                            __amdgpu_buffer_rsrc_t (&rc)[3]) {
+                                            __amdgpu_buffer_rsrc_t (&rc)[3], bool fin, int fi) {
     constexpr int DX = REV ? -1 : 1;
     const int x = x0 + i * DX;
     T N[9][VS];
-    level_from_raw<T, VS>(cur, a, lane, r0, et, walls, x == a.flux_col && x >= xa && x < xb, owner, q, N);
+    // fin: the flux column is one of the sweep's outputs; level l reaches it at step fi + l - 1
+    level_from_raw<T, VS>(cur, a, lane, r0, et, walls, fin && i == fi, owner, q, N);
     if (i + 1 < nl1) {
         if (!SLAB) {  // the resources of the next column triple: one new column
             if (DX > 0) {
@@ -637,12 +638,12 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
 #pragma unroll
     for (int l = 2; l <= K; ++l) {
         const int c = x - (l - 1) * DX;
-        const bool mine = c >= xa && c < xb;  // implies made (see above)
-        const bool flux = mine && c == a.flux_col;
+        const bool flux = fin && i == fi + l - 1;
         T out[9][VS];
         const bool made = i >= 2 * (l - 1);
         if (made) level_from_window<T, VS, DX>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, owner, q, out);
-        if (made && l == K && mine && owner) {
+        // level K's columns of the made steps are exactly the sweep's outputs [xa, xb)
+        if (made && l == K && owner) {
             if (!SLAB) {
                 const __amdgpu_buffer_rsrc_t rd = col_rsrc<T>(a.dst + (long)c * a.L.col);
 #pragma unroll
@@ -703,11 +704,13 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
         rc[2] = col_rsrc(col_wrap(a, x0 + 1));
     }
     load_raw_periodic<T, VS, MODE, SLAB, K>(a, x0, row0, off, bot, top, cur, bo, rc);
+    const bool fin = a.flux_col >= xa && a.flux_col < xb;
+    const int fi = REV ? xb + K - 2 - a.flux_col : a.flux_col - xa + K - 1;  // step of level 1 at the flux column
     // (a main loop without the per-level `made` checks, after 2(K-1) window-filling iterations,
     // lets the compiler hoist the collide constants into registers: VGPR spills, 512 VGPRs)
     for (int i = 0; i < nl1; ++i)
         sweepk_iter<T, VS, MODE, K, SLAB, REV>(a, i, nl1, x0, xa, xb, row0, off, lane, r0, et, owner, bot, top, walls, WA,
-                                               WB, cur, q, bo, rc);
+                                               WB, cur, q, bo, rc, fin, fi);
     return q;
 }
 
