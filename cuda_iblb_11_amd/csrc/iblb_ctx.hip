@@ -142,6 +142,7 @@ struct iblb_ctx {
     // gaps and band columns outside the patch rows: the patch rows it gets wrong (no force) are
     // overwritten by the trapezoid's last level, which waits for it (ev_bd)
     int band_full = 1;
+    int band_tail_ds = 1;  // IBLB_BAND_TAIL_DS
     hipEvent_t ev_bd = nullptr;
     int band_npatch = 0, band_pt_off = 0;  // patches; their table in d_band (BAND_PT ints each)
     char* s_alloc = nullptr;             // two scratch population buffers of the trapezoid
@@ -923,7 +924,7 @@ int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
         if (rc) return rc;
         HIP_TRY(c, launch_sweepk<T>(d, K, false, ds));
         if ((rc = ev_end(c, ev, EV_SWEEPK, (long long)n * c->ny, ds))) return rc;
-        if (c->band_st) HIP_TRY(c, hipEventRecord(c->ev_bd, ds));
+        if (c->band_st && !c->band_tail_ds) HIP_TRY(c, hipEventRecord(c->ev_bd, ds));
         return IBLB_OK;
     }
     if (c->band_nsweep <= 0) return IBLB_OK;
@@ -1008,11 +1009,23 @@ int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool slab, h
         a.variant = c->variant;
         // full deep sweep: it wrote (force-free) values into the patch rows of g^{t+K} too; the
         // last level overwrites them after it
-        if (j == K - 1 && band_full_deep(c) && bs != ds) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_bd, 0));
+        // (IBLB_BAND_TAIL_DS, default: the last level runs on the deep sweep's stream right behind
+        // it, once the chain's IB of that level is done: one cross-stream hop less on the cycle's
+        // critical path, and the deep stream's CUs)
+        hipStream_t ls = bs;
+        if (j == K - 1 && band_full_deep(c) && bs != ds) {
+            if (c->band_tail_ds) {
+                HIP_TRY(c, hipEventRecord(c->ev_bd, bs));
+                HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_bd, 0));
+                ls = ds;
+            } else {
+                HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_bd, 0));
+            }
+        }
         size_t ev = 0;
-        if ((rc = ev_begin(c, &ev, bs))) return rc;
-        HIP_TRY(c, launch_fused<T>(a, bs));
-        if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * a.nchl * 64 * c->V, bs))) return rc;
+        if ((rc = ev_begin(c, &ev, ls))) return rc;
+        HIP_TRY(c, launch_fused<T>(a, ls));
+        if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * a.nchl * 64 * c->V, ls))) return rc;
     }
     return IBLB_OK;
 }
@@ -1360,6 +1373,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_fused = (int)env_long("IBLB_BAND_FUSED", 0);
     c->band_full = (int)env_long("IBLB_BAND_FULL", 1);
+    c->band_tail_ds = (int)env_long("IBLB_BAND_TAIL_DS", 1);
     // halo buffers: recv_left, recv_right, send_left, send_right; each 10 (2-step) or 21 (IB)
     // slots + guards
     {
