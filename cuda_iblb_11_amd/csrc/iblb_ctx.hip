@@ -142,6 +142,11 @@ struct iblb_ctx {
     // gaps and band columns outside the patch rows: the patch rows it gets wrong (no force) are
     // overwritten by the trapezoid's last level, which waits for it (ev_bd)
     int band_full = 1;
+    // the launches read the plan's tables straight from its pinned slot (IBLB_BAND_HOSTTAB,
+    // default): a new plan of moving points costs no copy on the cycle's critical path
+    int band_hosttab = 1;
+    int* band_tab = nullptr;   // the tables the cycle's launches read (d_band or a pinned slot)
+    int band_pin_cur = -1;     // the pinned slot band_tab points into (its event: the cycle's end)
     int band_tail_ds = 1;  // IBLB_BAND_TAIL_DS
     hipEvent_t ev_bd = nullptr;
     int band_npatch = 0, band_pt_off = 0;  // patches; their table in d_band (BAND_PT ints each)
@@ -822,7 +827,7 @@ int band_step(iblb_ctx* c) {
         FusedArgs<T>& a = ba.f;
         a.L = c->L;
         for (int p = 0; p < 3; ++p) a.send_left[p] = a.send_right[p] = nullptr;
-        a.cols = c->d_band;
+        a.cols = c->band_tab;
         a.nch = c->nch;
         a.row_tab = 1;
         a.flags = c->flags;
@@ -849,7 +854,7 @@ int band_step(iblb_ctx* c) {
             }
         }
         ba.H0 = halo_at<T>(c, A);
-        ba.pt = c->d_band + c->band_pt_off;
+        ba.pt = c->band_tab + c->band_pt_off;
         ba.npatch = c->band_npatch;
         ba.K = K;
         ba.ib0 = c->ib_state == IB_PENDING;
@@ -890,6 +895,8 @@ int band_step(iblb_ctx* c) {
         c->send_sweep = false;
         c->send_deep = K;
     }
+    // the pinned table slot may be reused once every launch of this cycle has read it
+    if (c->band_pin_cur >= 0) HIP_TRY(c, hipEventRecord(c->band_pin_ev[c->band_pin_cur], c->stream));
     c->cur = 1 - c->cur;
     c->t += K;
     c->halo_valid = false;
@@ -929,7 +936,7 @@ int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     }
     if (c->band_nsweep <= 0) return IBLB_OK;
     Sweep2Args<T> d = sweep_args<T>(c, 0, 1, c->ncol, c->band_nsweep, std::max(1, c->deep_w));
-    d.sweep_tab = c->d_band + c->band_sweep_off;
+    d.sweep_tab = c->band_tab + c->band_sweep_off;
     d.tab_rows = 1;
     d.vs = c->deep_vs;
     d.variant = c->deep_variant;
@@ -990,7 +997,7 @@ int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool slab, h
         a.L = c->L;
         a.H = halo_at<T>(c, src);
         for (int p = 0; p < 3; ++p) a.send_left[p] = a.send_right[p] = nullptr;
-        a.cols = c->d_band;
+        a.cols = c->band_tab;
         a.col_begin = c->band_off[j];
         a.col_step = 1;
         a.ncols = c->band_n[j];
@@ -1373,6 +1380,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_fused = (int)env_long("IBLB_BAND_FUSED", 0);
     c->band_full = (int)env_long("IBLB_BAND_FULL", 1);
+    c->band_hosttab = (int)env_long("IBLB_BAND_HOSTTAB", 1);
     c->band_tail_ds = (int)env_long("IBLB_BAND_TAIL_DS", 1);
     // halo buffers: recv_left, recv_right, send_left, send_right; each 10 (2-step) or 21 (IB)
     // slots + guards
@@ -1756,9 +1764,18 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     if (c->band_pin_ev[slot]) HIP_TRY(c, hipEventSynchronize(c->band_pin_ev[slot]));
     else HIP_TRY(c, hipEventCreateWithFlags(&c->band_pin_ev[slot], hipEventDisableTiming));
     std::memcpy(c->band_pin[slot], tab.data(), tab.size() * sizeof(int));
-    HIP_TRY(c, hipMemcpyAsync(c->d_band, c->band_pin[slot], tab.size() * sizeof(int), hipMemcpyHostToDevice,
-                              c->stream));
-    HIP_TRY(c, hipEventRecord(c->band_pin_ev[slot], c->stream));
+    if (c->band_hosttab) {
+        // the kernels read the slot itself (device-accessible pinned memory); band_step records
+        // the slot's event after each cycle that reads it
+        c->band_tab = c->band_pin[slot];
+        c->band_pin_cur = slot;
+    } else {
+        HIP_TRY(c, hipMemcpyAsync(c->d_band, c->band_pin[slot], tab.size() * sizeof(int), hipMemcpyHostToDevice,
+                                  c->stream));
+        HIP_TRY(c, hipEventRecord(c->band_pin_ev[slot], c->stream));
+        c->band_tab = c->d_band;
+        c->band_pin_cur = -1;
+    }
     if (!c->s_alloc) {  // the trapezoid's scratch levels: two buffers laid out like g
         const size_t bytes = (size_t)(2 * c->buf_elems + c->buf_gap + 2 * GUARD) * c->esize;
         rc = alloc_zero(c, (void**)&c->s_alloc, bytes);
