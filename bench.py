@@ -43,7 +43,7 @@ WORKLOADS = {
     "K2": (2048, 2048, "f64", None, "K2: 2048x2048 D2Q9 channel, no IB"),
     "K3": (2048, 2048, "f64", "filament", "K3: 2048x2048 channel + one 256-point filament"),
     "K4": (8192, 2048, "f64", None, "K4: 8192x2048 channel, no IB"),
-    "K5": (8192, 2048, "f32", "array", "K5: 8192x2048 channel + 64 filaments x 96 points"),
+    "K5": (8192, 2048, "f32", "array", "K5: 8192x2048 channel + 64 filaments x 96 points, one on every slab edge"),
 }
 
 
@@ -51,13 +51,14 @@ def workload_points(kind, nx):
     """Lagrangian points of iteration `it` (a function), IB evaluated every iteration:
     K3: one 256-point filament at x = nx/2, u_s = (U0 (k/255) sin(2 pi it/T), 0)
     changing every iteration; K5: 64 filaments x 96 points (W.filament_array) whose points move
-    every iteration (tilt up to 8 columns over the period T = 1000)."""
+    every iteration (tilt up to 8 columns over the period T = 1000), standing at m * 128: one on
+    every slab edge of 1, 2, 4 or 8 slabs, x = 0 included (they cross it while they tilt)."""
     from cuda_iblb_11_amd import workloads as W
     if kind == "filament":
         return lambda it: W.filament(it, n_points=256, x0=nx / 2 + 0.3, y0=1.0, dy=1.0, U0=1e-3, period=1000)
-    if kind == "array":  # 64 filaments per 8192 columns (a K5 slab of 1024 columns holds 8)
+    if kind == "array":  # 64 filaments per 8192 columns, one on every slab edge (BASELINE config 5)
         nf = max(1, round(64 * nx / 8192))
-        return lambda it: W.filament_array(it, nx, n_fil=nf, pts=96, period=1000)
+        return lambda it: W.filament_array(it, nx, n_fil=nf, pts=96, period=1000, x_offset=0.0)
     return None
 
 
@@ -110,7 +111,8 @@ def parse():
     p.add_argument("--rccl-self", action="store_true",
                    help="N=1 rehearsal of the multi-GPU schedule: the slab is its own RCCL neighbour")
     p.add_argument("--same-device", action="store_true",
-                   help="testing only: every rank uses device 0 (exercise the RCCL slab path on one GPU)")
+                   help="rehearsal of the N > 1 path on one GPU: every rank uses device 0 and runs its slab as "
+                        "an RCCL self ring (RCCL refuses two ranks of one communicator on one device)")
     return p.parse_args()
 
 
@@ -254,21 +256,28 @@ def main():
     if a.scaling == "weak":
         nx *= world
     precision = a.precision or wprec
-    points = workload_points(wpts, nx)
-    ns = 0 if points is None else points(0)[0].size // 2
     xb, xc = P.plan_slabs(nx, world)[rank]
-    lat = P.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=W.BODY_FORCE, device=local,
-                    x_begin=xb, x_count=xc if world > 1 else 0, max_points=ns)
+    # --same-device (N > 1 on one GPU): each rank runs its slab as a lattice of its own, periodic over
+    # a one-rank RCCL self ring — the per-rank kernels, streams and halo exchange of the N-GPU run,
+    # and this script's whole N > 1 path (process group, barriers, MAX reductions), without the
+    # transfers between GPUs.  The workload's points are those of a lattice of the slab's width (K5:
+    # 8 filaments per 1024 columns, one on the slab edge).
+    rehearsal = distributed and a.same_device
+    lnx = xc if rehearsal else nx
+    points = workload_points(wpts, lnx)
+    ns = 0 if points is None else points(0)[0].size // 2
+    lat = P.Lattice(lnx, ny, W.TAU, W.TAU2, precision=precision, body_force=W.BODY_FORCE, device=local,
+                    x_begin=0 if rehearsal else xb, x_count=xc if world > 1 and not rehearsal else 0, max_points=ns)
     rho, u = W.perturbed_state(nx, ny, W.SEED)
     lat.set_state(P.split_state(rho, 1, nx, ny, xb, xc), P.split_state(u, 2, nx, ny, xb, xc))
     del rho, u
-    if distributed:
+    if rehearsal or (a.rccl_self and not distributed):
+        os.environ["IBLB_RCCL_SELF"] = "1"
+        lat.attach_rccl(P.rccl_unique_id(), 1, 0)
+    elif distributed:
         uid = [P.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         lat.attach_rccl(uid[0], world, rank)
-    elif a.rccl_self:
-        os.environ["IBLB_RCCL_SELF"] = "1"
-        lat.attach_rccl(P.rccl_unique_id(), 1, 0)
     drv = Driver(lat, points, a.frozen)
 
     # prime: the clock of an idle GPU ramps up over the first ~0.1-1 s of load; a 20-step timed
@@ -279,7 +288,7 @@ def main():
     while True:
         go = time.perf_counter() - tp < a.prime_seconds
         if distributed:
-            flag = torch.tensor([1.0 if go else 0.0], device="cpu" if a.same_device else "cuda")
+            flag = torch.tensor([1.0 if go else 0.0], device="cpu" if rehearsal else "cuda")
             dist.broadcast(flag, src=0)
             go = bool(flag.item() > 0)
         if not go:
@@ -320,16 +329,12 @@ def main():
         lat.synchronize()
         tm = lat.timing(reset=True)
         lat.set_profiling(False)
-    red_dev = "cpu" if a.same_device else "cuda"
+    red_dev = "cpu" if rehearsal else "cuda"
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        fl = torch.tensor([tm["fused_ms"] / max(tm["fused_launches"], 1)], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(fl, op=dist.ReduceOp.MAX)
-        launch_ms = float(fl.item())
-    else:
-        launch_ms = tm["fused_ms"] / max(tm["fused_launches"], 1)
+    launch_ms = tm["fused_ms"] / max(tm["fused_launches"], 1)
     # cells one timed launch updates (N > 1 overlapped: the interior columns of the slab)
     cells_per_launch = tm["fused_cells"] // max(tm["fused_launches"], 1)
     # dominant kernel: the two-iteration sweep where it runs (no IB owed between iterations).
@@ -341,18 +346,22 @@ def main():
     iters_per_launch = 1
     if sweep:
         launch_ms = tm["sweep_ms"] / tm["sweep_launches"]
-        if distributed:
-            sl = torch.tensor([launch_ms], dtype=torch.float64, device=red_dev)
-            dist.all_reduce(sl, op=dist.ReduceOp.MAX)
-            launch_ms = float(sl.item())
         cells_per_launch = tm["sweep_cells"] // tm["sweep_launches"]
         iters_per_launch = 2
-    # K >= 3 iterations per launch (lone slab, IBLB_SWEEP_DEPTH=K)
+    # K >= 3 iterations per launch (IBLB_SWEEP_DEPTH=K)
     if tm["sweepk_launches"] > 0 and tm["sweepk_ms"] >= max(tm["sweep_ms"], tm["fused_ms"]):
         sweep = int(tm["sweepk_depth"])
         launch_ms = tm["sweepk_ms"] / tm["sweepk_launches"]
         cells_per_launch = tm["sweepk_cells"] // tm["sweepk_launches"]
         iters_per_launch = sweep
+    if a.no_profile_events:  # nothing timed per launch: name the kernel the configuration runs
+        sweep = max(2, min(6, int(os.environ.get("IBLB_SWEEP_DEPTH", "5"))))
+        iters_per_launch = sweep
+        launch_ms, cells_per_launch = 0.0, 0
+    if distributed:
+        sl = torch.tensor([launch_ms], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(sl, op=dist.ReduceOp.MAX)
+        launch_ms = float(sl.item())
 
     # sanity: the state must stay finite (macro() is collective for an RCCL group)
     rho_s, _ = lat.macro()
@@ -402,8 +411,10 @@ def main():
                             + ("; IB band cycle: columns within K-1 of a forced column one iteration per launch, "
                                "the rest in the deep sweep" if ns and tm["sweepk_launches"] else ""),
                 "nx": nx, "ny": ny, "global_cells": cells, "ib_points": ns,
-                "parallelism": f"x-slab x{world}" + (" (RCCL halo)" if world > 1 else "")
-                               + (" (RCCL self-ring rehearsal)" if a.rccl_self and world == 1 else ""),
+                "parallelism": f"x-slab x{world}" + (" (RCCL halo)" if world > 1 and not rehearsal else "")
+                               + (" (RCCL self-ring rehearsal)" if a.rccl_self and world == 1 else "")
+                               + (" (same-device rehearsal: every rank a self ring over its slab on GPU 0)"
+                                  if rehearsal else ""),
             },
             "ib_ms_per_step": round(tm["ib_ms"] / a.steps, 5) if ns else None,
             # IB band cycle (K iterations per cycle): lattice updates done by one-step launches over
@@ -423,9 +434,12 @@ def main():
                 "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
                 "kernel": (f"sweepk_kernel<K={iters_per_launch}> (lbm_sweep_impl.h): {iters_per_launch} iterations per "
-                           "launch, state read and written once" if iters_per_launch > 2 else
+                           "launch, state read and written once"
+                           + (" (slab interior; boundary sweeps on the comm stream)" if world > 1 or a.rccl_self else "")
+                           if iters_per_launch > 2 else
                            "sweep2_kernel (lbm_sweep_impl.h): two iterations per launch, state read and written once"
-                           if sweep else "fused_kernel (lbm_kernels.hip)"),
+                           if sweep else "fused_kernel (lbm_kernels.hip)")
+                          + (" — not timed (--no-profile-events)" if a.no_profile_events else ""),
                 "bytes_per_cell": bytes_per_cell,
                 "cells_per_launch": cells_per_launch,
                 "iterations_per_launch": iters_per_launch,
@@ -434,8 +448,10 @@ def main():
                 "one_step_equivalent_gbps": round(mlups * 1e6 * bytes_per_cell / 1e9, 1),
                 "one_step_equivalent_frac": round(mlups * 1e6 * bytes_per_cell / 1e9 / HBM_PEAK_GBPS, 4),
                 "launch_ms": round(launch_ms, 5),
-                "launch_timing": ("HIP events in the timed region" if events_in_timed else
-                                  f"HIP events over {min(a.steps, 100)} further steps after the timed region"),
+                "launch_timing": ("none (--no-profile-events)" if a.no_profile_events else
+                                  "HIP events in the timed region" if events_in_timed else
+                                  f"HIP events over {min(a.steps, 100)} further steps after the timed region"
+                                  + (" (MAX over ranks)" if distributed else "")),
                 "traffic_source": traffic_src,
             },
             # the temporally blocked kernels are bound by vector issue, not HBM: their fp64 / fp32

@@ -1,5 +1,4 @@
-// ib_device.h — per-point immersed-boundary bodies shared by the IB kernels (ib_kernels.hip) and
-// the fused band-chain kernel (lbm_kernels.hip).
+// ib_device.h — per-point immersed-boundary bodies of the IB kernels (ib_kernels.hip).
 //
 // Reference: ImmersedBoundary.cu:94-133 (interpolate), :138-267 (spread).  The 3-point delta is
 // zero unless |x-xs| < 1.5 and |y-ys| < 1.5, so a point only touches the 3x3 nodes around
@@ -18,14 +17,16 @@ constexpr int LANES_PER_POINT = 16;
 __device__ __forceinline__ int node_x0(float xs) { return (int)nearbyint((double)xs); }
 
 // node (x, y) of a point's 3x3 spread, clipped to the lattice (no periodic image, as the
-// reference's cell-centric gather) and to this slab's columns
+// reference's cell-centric gather) and to the local columns [xlo, xhi) (default: the slab's own;
+// x_begin: the global column of local column 0 in the caller's image)
 __device__ __forceinline__ void spread_node(const Layout& L, int nx, int x_begin, int x, int y, float xs, float ys,
                                             float Fx, float Fy, int e, double* __restrict__ fd, long fplane,
-                                            uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
+                                            uint8_t* __restrict__ flags, int nch, int rows_per_chunk, int xlo = 0,
+                                            int xhi = -1) {
 #pragma clang fp contract(off)
     if (e == 0 || x < 0 || x >= nx || y < 0 || y >= L.ny) return;
     const int xc = x - x_begin;
-    if (xc < 0 || xc >= L.ncol) return;
+    if (xc < xlo || xc >= (xhi < 0 ? L.ncol : xhi)) return;
     const float del = d_delta(xs, ys, x, y);
     if (del == 0.f) return;
     const long o = (long)xc * L.rows + y;
@@ -100,70 +101,77 @@ __device__ __forceinline__ void ib_point_group(const T* __restrict__ g, const La
     spread_node(L, nx, 0, x, y, xs, ys, Fx, Fy, eps ? eps[k] : 1, fd, fplane, flags, nch, rows_per_chunk);
 }
 
-// Slab of a group: every slab evaluates, by itself, each point that spreads into it — the point's
-// nine nodes lie within 2 columns of the slab and are pulled through the IB halo (IbHalo) — and
-// spreads into its own columns.  A point straddling two slabs is evaluated by both with the same
-// data in the same order, so the force is bit-identical to a single slab; F_s is reported by the
-// slab holding column min(x0, XDIM-1) (zeros elsewhere: the reader sums).  Needs the reference's
-// invariant 0 <= nearbyint(xs) <= XDIM (boundary_check, main.cu:202-205).
-// part: 0 every point, 1 the inner points (x_begin+2 <= x0 <= x_begin+ncol-3: nodes and their
-// pulls inside the slab, no halo; they spread into columns >= 1 and <= ncol-2 only), 2 the others
-// (need the IB halo; they spread into columns <= 2 and >= ncol-3 only).
+// A slab with ghost columns (IbGhost, iblb_kernels.h): every slab evaluates, by itself, each point
+// that spreads into its columns [clo, chi) — its own columns (one-step IB) or also the ghost
+// columns an IB band trapezoid advances redundantly (band cycle) — from the columns it holds.
+//
+// Images: a point at node column x0 (global) appears at local column x0 - x_begin + m*nx for
+// m = -1, 0, 1 (the x-periodic copies a slab's ghost columns hold; a lone slab's ghosts hold its
+// own edge columns).  Each image spreads into its cells like the original (global columns clipped
+// to [0, XDIM): the reference's cell-centric spread has no periodic image,
+// ImmersedBoundary.cu:178-231).  The reference's flat-index quirk (ImmersedBoundary.cu:119-122:
+// node j = y*XDIM + x without wrap, so x = -1 reads column XDIM-1 of row y-1, x = XDIM column 0
+// of row y+1) is, in image coordinates, a pull from the node's own local column at row
+// j / XDIM: the local column of global XDIM-1 next to local column x0-1 = -1 - x_begin + m*nx is
+// that column itself.  A point straddling two slabs is evaluated by both from the same data in the
+// same order; the force differs from a single slab's only by the arrival order of the spread
+// atomics.  Every lane of the 16-lane group must call it (shuffles); pt and k are uniform over it.
 template <typename T>
-__device__ __forceinline__ void ib_slab_group(const T* __restrict__ g, const Layout& L, const IbHalo<T>& X, int nx,
-                                              int x_begin, bool pt, int k, int n, const float* __restrict__ s,
-                                              const float* __restrict__ u_s, const int* __restrict__ eps,
-                                              float* __restrict__ F_s, double* __restrict__ fd, long fplane,
-                                              uint8_t* __restrict__ flags, int nch, int rows_per_chunk, int part) {
+__device__ __forceinline__ void ib_ghost_group(const T* __restrict__ g, const Layout& L, const IbGhost& G, bool pt,
+                                               int k, int n, const float* __restrict__ s,
+                                               const float* __restrict__ u_s, const int* __restrict__ eps,
+                                               float* __restrict__ F_s, double* __restrict__ fd, long fplane,
+                                               uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
 #pragma clang fp contract(off)
     float xs = 0.f, ys = 0.f;
-    int x0 = 0, x = 0, y = 0;
-    bool mine = false, fs_here = true;  // fs_here: this call writes the point's F_s entry
+    int x0 = 0, y0 = 0;
+    bool own = false, go = false;
     if (pt) {
         xs = s[2 * k + 0];
         ys = s[2 * k + 1];
         x0 = node_x0(xs);
-        for (int dx = -1; dx <= 1; ++dx) {  // group-uniform: does the point spread into this slab?
-            const int xx = x0 + dx;
-            mine |= xx >= 0 && xx < nx && xx >= x_begin && xx < x_begin + L.ncol;
-        }
-        const bool inner = x0 >= x_begin + 2 && x0 <= x_begin + L.ncol - 3;
-        if (part == 1) fs_here = mine = mine && inner;
-        if (part == 2) {
-            fs_here = !(mine && inner);  // the edge launch also zeroes the points of other slabs
-            mine = mine && !inner;
+        y0 = node_x0(ys);
+        const int xo = x0 < G.nx - 1 ? x0 : G.nx - 1;
+        own = xo >= G.x_begin && xo < G.x_begin + L.ncol;
+        const int xl = x0 - G.x_begin;
+        const bool inner = xl >= 2 && xl <= L.ncol - 3;
+        go = G.part == 0 || (G.part == 1) == inner;
+        if (go && !own && n == 0) {  // another slab reports this point's F_s
+            F_s[2 * k + 0] = 0.f;
+            F_s[2 * k + 1] = 0.f;
         }
     }
-    double tx = 0., ty = 0.;
-    bool valid = false;
-    if (mine && n < 9) {
-        x = x0 + cx(n);
-        y = node_x0(ys) + cy(n);
-        const long j = (long)y * nx + x;
-        if (j >= 0 && j < (long)nx * L.ny) {
-            const int xj = (int)(j % nx), yj = (int)(j / nx);
-            int xl = xj - x_begin;  // slab-local node column, periodic
-            if (xl < -2) xl += nx;
-            else if (xl > L.ncol + 1) xl -= nx;
-            if (xl >= -2 && xl <= L.ncol + 1) {
+    const int e = pt ? (eps ? eps[k] : 1) : 0;
+    for (int m = -1; m <= 1; ++m) {
+        const int xl0 = x0 - G.x_begin + m * G.nx;
+        // group-uniform: does this image spread into [clo, chi)?
+        const bool img = go && (G.part != 1 || m == 0) && xl0 + 1 >= G.clo && xl0 - 1 < G.chi;
+        if (!img) continue;
+        double tx = 0., ty = 0.;
+        bool valid = false;
+        const int xn = xl0 + cx(n), x = x0 + cx(n), y = y0 + cy(n);
+        if (n < 9) {
+            const long j = (long)y * G.nx + x;  // flat index without wrap (ImmersedBoundary.cu:119-122)
+            if (j >= 0 && j < (long)G.nx * L.ny && xn - 1 >= -G.gc && xn + 1 < L.ncol + G.gc) {
+                const int yj = (int)(j / G.nx);
                 double f[9];
 #pragma unroll
-                for (int q = 0; q < 9; ++q) f[q] = Store<T>::to_f(pull_ib<T>(g, L, X, xl, yj, q), q);
+                for (int q = 0; q < 9; ++q) f[q] = Store<T>::to_f(pull_direct<T>(g, L, xn, yj, q), q);
                 node_term(f, xs, ys, x, y, u_s[2 * k + 0], u_s[2 * k + 1], tx, ty);
                 valid = true;
             }
         }
+        float Fx, Fy;
+        fold_terms(tx, ty, valid, Fx, Fy);
+        if (n == 0 && m == 0 && own) {
+            F_s[2 * k + 0] = Fx;
+            F_s[2 * k + 1] = Fy;
+        }
+        // local column of global column x in this image: x - (x_begin - m * nx) = xn
+        if (n < 9)
+            spread_node(L, G.nx, G.x_begin - m * G.nx, x, y, xs, ys, Fx, Fy, e, fd, fplane, flags, nch, rows_per_chunk,
+                        G.clo, G.chi);
     }
-    float Fx, Fy;
-    fold_terms(tx, ty, valid, Fx, Fy);
-    if (!pt || n >= 9) return;
-    if (n == 0 && fs_here) {
-        const int xo = x0 < nx - 1 ? x0 : nx - 1;
-        const bool owner = xo >= x_begin && xo < x_begin + L.ncol;
-        F_s[2 * k + 0] = owner ? Fx : 0.f;
-        F_s[2 * k + 1] = owner ? Fy : 0.f;
-    }
-    if (mine) spread_node(L, nx, x_begin, x, y, xs, ys, Fx, Fy, eps ? eps[k] : 1, fd, fplane, flags, nch, rows_per_chunk);
 }
 
 }  // namespace iblb

@@ -6,10 +6,10 @@
 //   w : 4/9    1/9 x4                        1/36 x4
 //
 // Slab layout in HBM (one context = one x-slab [x_begin, x_begin+ncol)):
-//   g[i*plane + xc*col + y]  — SoA, one plane per direction, y fastest, column stride
-//   `col` (>= ny, multiple of 64 elements), planes padded apart.  A column is
-//   contiguous, so the halo a slab exchanges (one column, 3 planes) is 3 contiguous
-//   runs and needs no packing pass.
+//   g[xc*col + i*plane + y]  — the nine planes of a column adjacent (plane = ny rounded up to
+//   whole waves), y fastest, columns contiguous.  A slab of a group keeps `gc` ghost columns
+//   on each side inside the same buffer (xc in [-gc, 0) and [ncol, ncol+gc)): its halo is
+//   one contiguous block of whole columns per side, sent and received by RCCL in place.
 //
 // State held between steps: post-collision populations f1^{t-1} ("g").  Streaming is a
 // PULL applied when g is read:
@@ -46,22 +46,17 @@ struct Layout {
     int ncol;    // columns in this slab
     long col;    // column stride of the populations (elements)
     long plane;  // plane stride of the populations (elements)
-    long rows;   // ny rounded up to whole waves: one halo slot, the column stride of the
-                 // dense force and boot fields (plane stride fplane = ncol * rows)
+    long rows;   // ny rounded up to whole waves: the column stride of the dense force and the
+                 // boot fields (plane stride fplane)
 };
 
 // Pointers to the three halo planes of column -1 (left, planes 1,5,8) and column
-// ncol (right, planes 3,6,7).  Single slab: they point into g itself (periodic wrap).
+// ncol (right, planes 3,6,7).  Lone slab: they point into g itself (periodic wrap); slab of a
+// group: into its ghost columns -1 and ncol.
 template <typename T>
 struct Halo {
     const T* left[3];
     const T* right[3];
-};
-
-template <typename T>
-struct SendPtrs {
-    T* left[3];   // planes {3,6,7} of column 0
-    T* right[3];  // planes {1,5,8} of column ncol-1
 };
 
 // Relaxation and forcing constants shared by every collide.
@@ -91,84 +86,14 @@ __device__ __forceinline__ T pull(const T* __restrict__ g, const Layout& L, cons
     return g[k * L.plane + (long)sx * L.col + sy];
 }
 
-// ---- IB halo (multi-slab immersed boundary) ------------------------------------------------
-// A slab computes the nodes of every point that spreads into it itself: node columns reach
-// 2 beyond the slab, their pulls 3 beyond.  With IB the halo buffers hold IB_HALO_SLOTS
-// columns-planes per side (received from the neighbour, in this slot order):
-//   left  (from the left neighbour):  0-2 col -1 planes {1,5,8} (the streaming halo)
-//                                     3-8 col -1 planes {0,2,3,4,6,7}
-//                                     9-17 col -2 planes 0..8,  18-20 col -3 planes {1,5,8}
-//   right (from the right neighbour): 0-2 col ncol planes {3,6,7}, 3-8 col ncol planes
-//                                     {0,1,2,4,5,8}, 9-17 col ncol+1 planes 0..8,
-//                                     18-20 col ncol+2 planes {3,6,7}
-constexpr int HALO_SLOTS = 3;
-constexpr int IB_HALO_SLOTS = 21;
-__host__ __device__ constexpr int left_other(int i) {   // planes of col -1 not in {1,5,8}
-    return i == 0 ? 0 : (i == 1 ? 2 : (i == 2 ? 3 : (i == 3 ? 4 : (i == 4 ? 6 : 7))));
-}
-__host__ __device__ constexpr int right_other(int i) {  // planes of col ncol not in {3,6,7}
-    return i == 0 ? 0 : (i == 1 ? 1 : (i == 2 ? 2 : (i == 3 ? 4 : (i == 4 ? 5 : 8))));
-}
-// slot of plane k of the d-th column beyond the slab edge (d = 0, 1, 2) in the left / right
-// buffer; -1 if that plane is not carried
-__host__ __device__ constexpr int ib_slot(bool left, int d, int k) {
-    if (d == 1) return 9 + k;
-    const bool streamed = left ? cx(k) == 1 : cx(k) == -1;
-    if (d == 2) return streamed ? 18 + halo_slot(k) : -1;
-    if (streamed) return halo_slot(k);
-    for (int i = 0; i < 6; ++i)
-        if ((left ? left_other(i) : right_other(i)) == k) return 3 + i;
-    return -1;
-}
-// the sender's view: (column offset from its edge, plane) of slot s of the buffer it sends
-// to its right neighbour (its last columns) / to its left neighbour (its first columns)
-__host__ __device__ constexpr int send_slot_depth(int s) { return s < 9 ? 0 : (s < 18 ? 1 : 2); }
-__host__ __device__ constexpr int send_slot_plane(bool to_right, int s) {
-    return s < 3 ? (to_right ? left_plane(s) : right_plane(s))
-                 : (s < 9 ? (to_right ? left_other(s - 3) : right_other(s - 3))
-                          : (s < 18 ? s - 9 : (to_right ? left_plane(s - 18) : right_plane(s - 18))));
-}
-
-// ---- deep halo (K-iteration sweeps across slabs, K = 3 .. 6) --------------------------------
-// The IB halo generalised to depth K: d = 0 as ib_slot (streamed planes first, so slots 0-2 are
-// the one-step halo), d = 1 .. K-2 all nine planes, d = K-1 the streamed planes only.  For K = 3
-// it is exactly the IB halo.
-__host__ __device__ constexpr int deep_slots(int K) { return 9 * (K - 1) + 3; }
-__host__ __device__ constexpr int deep_slot(bool left, int d, int k, int K) {
-    if (d == 0) return ib_slot(left, 0, k);
-    if (d < K - 1) return 9 * d + k;
-    const bool streamed = left ? cx(k) == 1 : cx(k) == -1;
-    return (d == K - 1 && streamed) ? 9 * (K - 1) + halo_slot(k) : -1;
-}
-// the sender's view of slot s: column offset d from its edge and plane
-__host__ __device__ constexpr int deep_send_depth(int s, int K) { return s < 9 ? 0 : (s < 9 * (K - 1) ? s / 9 : K - 1); }
-__host__ __device__ constexpr int deep_send_plane(bool to_right, int s, int K) {
-    return s < 9 ? send_slot_plane(to_right, s)
-                 : (s < 9 * (K - 1) ? s % 9 : (to_right ? left_plane(s - 9 * (K - 1)) : right_plane(s - 9 * (K - 1))));
-}
-
+// Pull of f^t(xl, y, k) from a buffer whose columns xl-1 .. xl+1 are all present: the slab's own
+// columns or its ghost columns (a slab of a group holds `gc` ghost columns on each side, filled
+// from the neighbours; a lone slab fills them with periodic copies when a band cycle needs them).
 template <typename T>
-struct IbHalo {
-    const T* left;   // received from the left neighbour, IB_HALO_SLOTS slots of `col` elements
-    const T* right;  // received from the right neighbour
-};
-
-// column xl (-3 .. ncol+2) of plane k
-template <typename T>
-__device__ __forceinline__ const T* ib_col(const T* __restrict__ g, const Layout& L, const IbHalo<T>& X, int xl,
-                                           int k) {
-    if (xl < 0) return X.left + (long)ib_slot(true, -1 - xl, k) * L.rows;
-    if (xl >= L.ncol) return X.right + (long)ib_slot(false, xl - L.ncol, k) * L.rows;
-    return g + k * L.plane + (long)xl * L.col;
-}
-
-// pull of f^t(xl, y, k) for a node column xl in [-2, ncol+1] (same rules as pull())
-template <typename T>
-__device__ __forceinline__ T pull_ib(const T* __restrict__ g, const Layout& L, const IbHalo<T>& X, int xl, int y,
-                                     int k) {
-    if (y == 0 && cy(k) == 1) return ib_col(g, L, X, xl, k == 2 ? 4 : (k == 5 ? 7 : 8))[0];
-    if (y == L.ny - 1 && cy(k) == -1) return ib_col(g, L, X, xl, k == 4 ? 2 : (k == 8 ? 5 : 6))[y];
-    return ib_col(g, L, X, xl - cx(k), k)[y - cy(k)];
+__device__ __forceinline__ T pull_direct(const T* __restrict__ g, const Layout& L, int xl, int y, int k) {
+    if (y == 0 && cy(k) == 1) return g[(k == 2 ? 4 : (k == 5 ? 7 : 8)) * L.plane + (long)xl * L.col];
+    if (y == L.ny - 1 && cy(k) == -1) return g[(k == 4 ? 2 : (k == 8 ? 5 : 6)) * L.plane + (long)xl * L.col + y];
+    return g[k * L.plane + (long)(xl - cx(k)) * L.col + (y - cy(k))];
 }
 
 // Storage conversion: double planes hold f, float planes hold the deviation f - w_i.

@@ -12,12 +12,10 @@
 namespace iblb {
 
 // One wave = one (column, chunk of 64*V rows); lane l owns rows y0 .. y0+V-1.
-// Column-uniform decisions (halo source, flux column, IB flag, send buffers) are
-// scalar branches.  Walls are per-lane fixes of the first / last row.
-// fused_wave: the body of one wave (gw = its global wave index in the launch); fused_kernel runs
-// one per wave, band_kernel loops its waves over a patch's entries level by level.
-// VE: the wave-uniform loads (wall rows, chunk-edge rows, the IB flag) as vector loads (vofs)
-template <typename T, int V, bool IB, int MODE, bool VE = false>
+// Column-uniform decisions (halo source, flux column, IB flag) are scalar branches.  Walls are
+// per-lane fixes of the first / last row.  Columns outside [0, ncol) (IB band trapezoids over a
+// slab's ghost columns) are addressed directly.
+template <typename T, int V, bool IB, int MODE>
 __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, const int lane) {
     typedef typename VT<T, V>::type vec;
     typedef typename Calc<T>::R R;
@@ -62,22 +60,22 @@ __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, 
     vec v0 = ld_plane<T, V, MODE>(p0 + y0);
     vec v1 = ld_plane<T, V, MODE>(p1 + y0);
     vec v3 = ld_plane<T, V, MODE>(p3 + y0);
-    vec v2 = ld_shifted<T, V, MODE, +1, VE>(p2, y0, cs, lane);
-    vec v5 = ld_shifted<T, V, MODE, +1, VE>(p5, y0, cs, lane);
-    vec v6 = ld_shifted<T, V, MODE, +1, VE>(p6, y0, cs, lane);
-    vec v4 = ld_shifted<T, V, MODE, -1, VE>(p4, y0, cs, lane);
-    vec v7 = ld_shifted<T, V, MODE, -1, VE>(p7, y0, cs, lane);
-    vec v8 = ld_shifted<T, V, MODE, -1, VE>(p8, y0, cs, lane);
+    vec v2 = ld_shifted<T, V, MODE, +1>(p2, y0, cs, lane);
+    vec v5 = ld_shifted<T, V, MODE, +1>(p5, y0, cs, lane);
+    vec v6 = ld_shifted<T, V, MODE, +1>(p6, y0, cs, lane);
+    vec v4 = ld_shifted<T, V, MODE, -1>(p4, y0, cs, lane);
+    vec v7 = ld_shifted<T, V, MODE, -1>(p7, y0, cs, lane);
+    vec v8 = ld_shifted<T, V, MODE, -1>(p8, y0, cs, lane);
     if (y0 == 0) {  // bounce-back on y = 0 (LatticeBoltzmann.cu:328-340)
-        v2[0] = src[vofs<VE>(4 * L.plane + cb)];
-        v5[0] = src[vofs<VE>(7 * L.plane + cb)];
-        v6[0] = src[vofs<VE>(8 * L.plane + cb)];
+        v2[0] = src[(4 * L.plane + cb)];
+        v5[0] = src[(7 * L.plane + cb)];
+        v6[0] = src[(8 * L.plane + cb)];
     }
     const int et = L.ny - 1 - y0;
     if (et >= 0 && et < V) {  // same-cell mirror on y = Y-1 (LatticeBoltzmann.cu:341-353)
         const long top = cb + L.ny - 1;
-        const T t2 = src[vofs<VE>(2 * L.plane + top)], t5 = src[vofs<VE>(5 * L.plane + top)],
-                t6 = src[vofs<VE>(6 * L.plane + top)];
+        const T t2 = src[(2 * L.plane + top)], t5 = src[(5 * L.plane + top)],
+                t6 = src[(6 * L.plane + top)];
 #pragma unroll
         for (int e = 0; e < V; ++e)
             if (e == et) { v4[e] = t2; v8[e] = t5; v7[e] = t6; }
@@ -85,7 +83,7 @@ __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, 
 
     // dense IB force for this (column, chunk), consumed and cleared
     bool has_f = false;
-    if (IB) has_f = a.flags[vofs<VE>((long)xc * a.nch + ch)] != 0;
+    if (IB) has_f = a.flags[((long)xc * a.nch + ch)] != 0;
     double fxv[V], fyv[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) { fxv[e] = 0.; fyv[e] = 0.; }
@@ -130,16 +128,6 @@ __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, 
                 dst[e + 6 * L.plane] = v6[e]; dst[e + 7 * L.plane] = v7[e]; dst[e + 8 * L.plane] = v8[e];
             }
     }
-    if (xc == 0 && a.send_left[0]) {
-        sta<T, V>(a.send_left[0] + y0, v3);
-        sta<T, V>(a.send_left[1] + y0, v6);
-        sta<T, V>(a.send_left[2] + y0, v7);
-    }
-    if (xc == L.ncol - 1 && a.send_right[0]) {
-        sta<T, V>(a.send_right[0] + y0, v1);
-        sta<T, V>(a.send_right[1] + y0, v5);
-        sta<T, V>(a.send_right[2] + y0, v8);
-    }
     if (do_flux) {
         q = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, q);
@@ -179,122 +167,12 @@ hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s) {
     }
 }
 
-// ---- the band chain of an IB band cycle in one launch (BandArgs, iblb_kernels.h) ----------
-// Workgroup q = patch q, BAND_WAVES waves.  Between the phases of a level every wave's global
-// stores and atomics must be visible to the other waves of the workgroup: all of them run on one
-// CU, whose vector L1 is write-through and kept coherent with the CU's own stores and atomics, so
-// the workgroup barrier (__syncthreads: release / acquire at workgroup scope = wait for the
-// wave's memory operations) suffices.  An agent-scope fence would write back and invalidate the
-// XCD's whole L2 at every barrier (buffer_wbl2 / buffer_inv sc1 on gfx950: the XCDs' L2s are not
-// coherent with each other) and stall the deep sweep running beside it.  Wave-uniform loads of
-// data the kernel writes itself go through vofs (vector loads): the scalar data cache is not
-// coherent with vector stores.
-constexpr int BAND_WAVES = 16;
-constexpr int BAND_LIST = 4096;  // points of a patch listed per IB pass (LDS)
-
-__device__ __forceinline__ void band_sync() { __syncthreads(); }
-
-// a[j] for the wave-uniform level j without indexing the by-value argument (which would copy it
-// to scratch): a chain of scalar selects
-template <typename P>
-__device__ __forceinline__ P pick(const P (&a)[BAND_MAX_K], int j) {
-    P r = a[0];
-#pragma unroll
-    for (int i = 1; i < BAND_MAX_K; ++i) r = j == i ? a[i] : r;
-    return r;
-}
-
-template <typename T, int V, int MODE>
-__global__ __launch_bounds__(64 * BAND_WAVES) void band_kernel(BandArgs<T> a) {
-    __shared__ int list[BAND_LIST];
-    __shared__ int cnt;
-    const int q = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // (a slab without patches of its own still runs one workgroup: it zeroes the F_s of the
-    // points other slabs own)
-    const bool patch = q < a.npatch;
-    const int* pt = a.pt + q * BAND_PT;
-    const int xlo = patch ? pt[0] : 1, xhi = patch ? pt[1] : 0;
-    constexpr int NT = 64 * BAND_WAVES, NG = NT / LANES_PER_POINT;
-    for (int j = 0; j < a.K; ++j) {
-        const T* src = pick(a.src, j);
-        if (j > 0 || a.ib0) {
-            // IB of level j: list the points whose node column lies in the patch, then one 16-lane
-            // group per listed point (ib_device.h)
-            const float *ps = pick(a.ps, j), *pus = pick(a.pus, j);
-            const int* pe = pick(a.pe, j);
-            const Halo<T>& H = a.H0;  // only level 0's nodes can reach x = 0 (plan_bands_t)
-            for (int base = 0; base < a.ns;) {
-                if (tid == 0) cnt = 0;
-                __syncthreads();
-                while (base < a.ns && cnt + NT <= BAND_LIST) {
-                    const int k = base + tid;
-                    if (k < a.ns) {
-                        const int x0 = node_x0(ps[2 * k]);
-                        const int xl = x0 - a.x_begin;
-                        if (xl >= xlo && xl <= xhi) list[atomicAdd(&cnt, 1)] = k;
-                        if (a.slab && q == 0) {  // F_s of the points another slab owns: zero here
-                            const int xo = x0 < a.nx - 1 ? x0 : a.nx - 1;
-                            if (xo < a.x_begin || xo >= a.x_begin + a.f.L.ncol) {
-                                a.F_s[2 * k + 0] = 0.f;
-                                a.F_s[2 * k + 1] = 0.f;
-                            }
-                        }
-                    }
-                    base += NT;
-                    __syncthreads();
-                }
-                const int n = cnt;
-                for (int p0 = 0; p0 < n; p0 += NG) {
-                    const int p = p0 + tid / LANES_PER_POINT;
-                    const bool has = p < n;
-                    const int k = has ? list[p] : 0;
-                    if (a.slab)
-                        ib_slab_group<T>(src, a.f.L, a.X, a.nx, a.x_begin, has, k, tid % LANES_PER_POINT, ps, pus, pe,
-                                         a.F_s, a.f.fdense, a.f.fplane, a.f.flags, a.f.nch, a.rows_per_chunk, 0);
-                    else
-                        ib_point_group<T>(src, a.f.L, H, a.nx, has, k, tid % LANES_PER_POINT, ps, pus, pe, a.F_s,
-                                          a.f.fdense, a.f.fplane, a.f.flags, a.f.nch, a.rows_per_chunk);
-                }
-                band_sync();
-            }
-        }
-        // the one-step collide of the level's entries
-        FusedArgs<T> f = a.f;
-        f.src = src;
-        f.dst = pick(a.dst, j);
-        f.H = a.H0;
-        f.col_begin = patch ? pt[2 + 3 * j] : 0;
-        f.ncols = patch ? pt[3 + 3 * j] : 0;
-        f.nchl = patch ? pt[4 + 3 * j] : 1;
-        f.store_rows = j == a.K - 1;
-        const int items = f.ncols * f.nchl;
-        for (int gw = wave; gw < items; gw += BAND_WAVES) fused_wave<T, V, true, MODE, true>(f, gw, lane);
-        band_sync();
-    }
-}
-
-template <typename T>
-hipError_t launch_band(const BandArgs<T>& a, hipStream_t s) {
-    if (a.npatch <= 0 && !a.slab) return hipSuccess;
-    if (a.K < 1 || a.K > BAND_MAX_K) return hipErrorInvalidValue;
-    constexpr int V = vec_of<T>();
-    const unsigned nt = 64 * BAND_WAVES, nb = (unsigned)(a.npatch > 0 ? a.npatch : 1);
-    switch (a.f.variant) {
-        case 3: band_kernel<T, V, 3><<<nb, nt, 0, s>>>(a); break;
-        case 5: band_kernel<T, V, 5><<<nb, nt, 0, s>>>(a); break;
-        default: band_kernel<T, V, 0><<<nb, nt, 0, s>>>(a); break;
-    }
-    return hipGetLastError();
-}
-
 // ---- boot step: collide f^0 with given rho^0, u^0, force^0 (main.cu:720-754, it = 0) --
 template <typename T>
 __global__ __launch_bounds__(256) void boot_kernel(const T* __restrict__ src, T* __restrict__ dst, Layout L,
                                                    const double* __restrict__ rho0, const double* __restrict__ u0,
-                                                   const double* __restrict__ force0, long fplane, SendPtrs<T> sp,
-                                                   Coef c, KConst kc) {
+                                                   const double* __restrict__ force0, long fplane, Coef c,
+                                                   KConst kc) {
     typedef typename Calc<T>::R R;
     constexpr bool DEV = Store<T>::dev;
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -311,17 +189,13 @@ __global__ __launch_bounds__(256) void boot_kernel(const T* __restrict__ src, T*
     collide<R, DEV>(f, (R)rho, (R)(rho - 1.0), ux, uy, kb, make_kforce<R>(kb, Fx, Fy));
 #pragma unroll
     for (int i = 0; i < 9; ++i) dst[i * L.plane + o] = (T)f[i];
-    if (xc == 0 && sp.left[0]) { sp.left[0][y] = (T)f[3]; sp.left[1][y] = (T)f[6]; sp.left[2][y] = (T)f[7]; }
-    if (xc == L.ncol - 1 && sp.right[0]) { sp.right[0][y] = (T)f[1]; sp.right[1][y] = (T)f[5]; sp.right[2][y] = (T)f[8]; }
 }
 
 template <typename T>
 hipError_t launch_boot(const T* src, T* dst, Layout L, const double* rho0, const double* u0, const double* force0,
-                       long fplane, T* const send_left[3], T* const send_right[3], Coef c, KConst k, hipStream_t s) {
-    SendPtrs<T> sp;
-    for (int p = 0; p < 3; ++p) { sp.left[p] = send_left[p]; sp.right[p] = send_right[p]; }
+                       long fplane, Coef c, KConst k, hipStream_t s) {
     const long n = (long)L.ncol * L.ny;
-    boot_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(src, dst, L, rho0, u0, force0, fplane, sp, c, k);
+    boot_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(src, dst, L, rho0, u0, force0, fplane, c, k);
     return hipGetLastError();
 }
 
@@ -465,9 +339,8 @@ hipError_t launch_field_out(const double* lay, double* ref, Layout L, int ncomp,
 
 #define IBLB_INST(T)                                                                                            \
     template hipError_t launch_fused<T>(const FusedArgs<T>&, hipStream_t);                                      \
-    template hipError_t launch_band<T>(const BandArgs<T>&, hipStream_t);                                        \
     template hipError_t launch_boot<T>(const T*, T*, Layout, const double*, const double*, const double*, long,  \
-                                       T* const[3], T* const[3], Coef, KConst, hipStream_t);                            \
+                                       Coef, KConst, hipStream_t);                                                  \
     template hipError_t launch_macro_out<T>(const T*, Layout, Halo<T>, const double*, long, double, double,      \
                                             double*, double*, hipStream_t);                                     \
     template hipError_t launch_pop_out<T>(const T*, Layout, Halo<T>, double*, int, hipStream_t);                     \

@@ -25,9 +25,8 @@
 // Algorithmic HBM bytes per launch: one read + one write of the state = 144 B per cell (f64) for
 // TWO lattice updates, plus the (W+2)/W re-read of the sweep edges.
 //
-// Single slab: columns -2, -1, ncol, ncol+1 are the periodic images.  Slab of a group: they come
-// from the 2-step halo (9 planes per side, slots in iblb_device.h: SWEEP_HALO_SLOTS), and the
-// kernel writes the 9 planes its neighbours need into the send buffers.
+// Lone slab: columns -2, -1, ncol, ncol+1 are the periodic images.  Slab of a group (SLAB): they
+// are the ghost columns of the buffer itself, filled by the halo exchange (whole columns, in place).
 #pragma once
 
 #include "lbm_vec.h"
@@ -38,27 +37,26 @@ enum { MODE_NO_PREFETCH = 8 };  // sweep only (MODE bits 1, 2 as in lbm_vec.h)
 
 namespace {
 
-// pointer to plane k of column x (x in [-2, ncol+1]); x is wave-uniform.  Computed, not looked
-// up: a table of halo pointers in the kernel arguments costs more SGPRs than a wave has.
+// pointer to plane k of column x (x in [-2, ncol+1]); x is wave-uniform.  SLAB: ghost columns
+// in the buffer; else the periodic image.
 template <typename T, bool SLAB>
 __device__ __forceinline__ const T* sweep_col(const Sweep2Args<T>& a, int x, int k) {
     const Layout& L = a.L;
-    if (x >= 0 && x < L.ncol) return a.src + (long)x * L.col + (long)k * L.plane;
-    if (!SLAB) {  // lone slab: periodic image
-        const int xw = x < 0 ? x + L.ncol : x - L.ncol;
-        return a.src + (long)xw * L.col + (long)k * L.plane;
-    }
-    if (x < 0) return a.recv_left + (long)sweep_slot(true, -1 - x, k) * L.rows;
-    return a.recv_right + (long)sweep_slot(false, x - L.ncol, k) * L.rows;
+    if (SLAB || (x >= 0 && x < L.ncol)) return a.src + (long)x * L.col + (long)k * L.plane;
+    const int xw = x < 0 ? x + L.ncol : x - L.ncol;
+    return a.src + (long)xw * L.col + (long)k * L.plane;
 }
 
-// g0(x, y, k) for the wall cells (y = 0 or Y-1) of column x; a group slab's halo columns carry
-// the same-cell values their walls need in slot 9
+// g0(x, y, k) for the wall cells (y = 0 or Y-1) of column x
 template <typename T, bool SLAB>
 __device__ __forceinline__ T wall_val(const Sweep2Args<T>& a, int x, int k, int y) {
-    if (SLAB && x == -1 && (k == 7 || k == 6)) return a.recv_left[9 * a.L.rows + (y == 0 ? 0 : 1)];
-    if (SLAB && x == a.L.ncol && (k == 8 || k == 5)) return a.recv_right[9 * a.L.rows + (y == 0 ? 0 : 1)];
     return sweep_col<T, SLAB>(a, x, k)[y];
+}
+
+// a sampled flux row: inside the lattice and outside the rows an IB band patch accounts for
+template <typename T>
+__device__ __forceinline__ bool flux_row(const Sweep2Args<T>& a, int y) {
+    return y < a.L.ny && (y < a.fskip0 || y >= a.fskip1);
 }
 
 // rows y0 .. y0+VS-1 of plane pointer p shifted by one row: DIR = +1 -> rows y-1, DIR = -1 ->
@@ -236,7 +234,7 @@ __device__ __forceinline__ double sweep_walk(const Sweep2Args<T>& a, int xa, int
 #pragma unroll
                 for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
                 const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
-                if (flux1 && owner && r0 + e < L.ny) q += (double)ux / a.flux_norm;
+                if (flux1 && owner && flux_row(a, r0 + e)) q += (double)ux / a.flux_norm;
 #pragma unroll
                 for (int k = 0; k < 9; ++k) C[k][e] = (T)f[k];
             }
@@ -258,7 +256,7 @@ __device__ __forceinline__ double sweep_walk(const Sweep2Args<T>& a, int xa, int
 #pragma unroll
                 for (int k = 0; k < 9; ++k) f[k] = (R)s[k][e];
                 const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
-                if (flux2 && owner && r0 + e < L.ny) q += (double)ux / a.flux_norm;
+                if (flux2 && owner && flux_row(a, r0 + e)) q += (double)ux / a.flux_norm;
 #pragma unroll
                 for (int k = 0; k < 9; ++k) s[k][e] = (T)f[k];
             }
@@ -266,35 +264,6 @@ __device__ __forceinline__ double sweep_walk(const Sweep2Args<T>& a, int xa, int
                 T* dst = a.dst + (long)xo * L.col + row0;
 #pragma unroll
                 for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * L.plane, off, s[k]);
-                if (SLAB) {  // the 2-step halo of g^{t+2} for the neighbours (iblb_kernels.h)
-                    const bool sl0 = xo == 0, sl1 = xo == 1, sr0 = xo == L.ncol - 1, sr1 = xo == L.ncol - 2;
-                    if (sl0 || sl1 || sr0 || sr1) {
-                        T* buf = (sl0 || sl1) ? a.send_left + row0 : a.send_right + row0;
-                        const bool left = sl0 || sl1;
-                        const int s0 = (sl0 || sr0) ? 0 : 6;
-                        const int ns = (sl0 || sr0) ? 6 : 3;
-#pragma unroll
-                        for (int q = 0; q < 6; ++q) {
-                            if (q >= ns) break;
-                            const int sl = s0 + q;
-                            // slot sl carries plane sweep_send_plane(left, sl)
-                            T v[VS];
-#pragma unroll
-                            for (int k = 0; k < 9; ++k)
-                                if (k == (left ? sweep_send_plane(true, sl) : sweep_send_plane(false, sl)))
-#pragma unroll
-                                    for (int e = 0; e < VS; ++e) v[e] = s[k][e];
-                            st_rows<T, VS, 0>(buf + (long)sl * L.rows, off, v);
-                        }
-                        if (sl0 || sr0) {  // slot 9: the same-cell wall values of this column
-                            T* w = buf - row0 + 9 * L.rows;
-                            if (bot) w[0] = sl0 ? s[8][0] : s[7][0];
-#pragma unroll
-                            for (int e = 0; e < VS; ++e)
-                                if (top && e == et) w[1] = sl0 ? s[5][e] : s[6][e];
-                        }
-                    }
-                }
             }
         }
 
@@ -367,16 +336,11 @@ static hipError_t launch_sweep_mode(const Sweep2Args<T>& a, bool slab, unsigned 
     return hipGetLastError();
 }
 
+// (variant: nontemporal stores, software prefetch of the next column — the measured best of the
+// round-1 variants, profiles/r01p_tune_*.log; the others are no longer built)
 template <typename T, int VS>
 static hipError_t launch_sweep_vs(const Sweep2Args<T>& a, bool slab, unsigned blocks, hipStream_t s) {
-    switch (a.variant) {
-        case 1: return launch_sweep_mode<T, VS, 1>(a, slab, blocks, s);
-        case 2: return launch_sweep_mode<T, VS, 2>(a, slab, blocks, s);
-        case 3: return launch_sweep_mode<T, VS, 3>(a, slab, blocks, s);
-        case 8: return launch_sweep_mode<T, VS, 8>(a, slab, blocks, s);
-        case 9: return launch_sweep_mode<T, VS, 9>(a, slab, blocks, s);
-        default: return launch_sweep_mode<T, VS, 0>(a, slab, blocks, s);
-    }
+    return launch_sweep_mode<T, VS, MODE_NT_STORE>(a, slab, blocks, s);
 }
 
 template <typename T>
@@ -386,7 +350,6 @@ hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s) {
     // the 512-element guards of the buffers (iblb_ctx.hip)
     if (a.W <= 0 || a.L.ncol < 2 || a.vs <= 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 || a.L.col % a.vs != 0)
         return hipErrorInvalidValue;
-    if (slab && (!a.recv_left || !a.recv_right || !a.send_left || !a.send_right)) return hipErrorInvalidValue;
     a.nch = (a.L.ny + 62 * a.vs - 1) / (62 * a.vs);
     const unsigned blocks = a.map == 0 ? (unsigned)(((a.nsweep + 3) / 4) * (long)a.nch)
                                        : (unsigned)(((long)a.nsweep * a.nch + 3) / 4);
@@ -424,12 +387,10 @@ __device__ __forceinline__ const T* col_periodic(const Sweep2Args<T>& a, int x, 
 }
 
 // plane k of column x for the deep walk: a lone slab wraps periodically; a slab of a group
-// (SLAB) reads columns beyond its edges from the deep halo (deep_slot, K columns per side)
+// (SLAB) reads the ghost columns of its buffer (K of them per side after the halo exchange)
 template <typename T, bool SLAB, int K>
 __device__ __forceinline__ const T* col_deep(const Sweep2Args<T>& a, int x, int k) {
     if (!SLAB) return col_periodic<T>(a, x, k);
-    if (x < 0) return a.recv_left + (long)deep_slot(true, -1 - x, k, K) * a.L.rows;
-    if (x >= a.L.ncol) return a.recv_right + (long)deep_slot(false, x - a.L.ncol, k, K) * a.L.rows;
     return a.src + (long)x * a.L.col + (long)k * a.L.plane;
 }
 
@@ -456,6 +417,11 @@ __device__ __forceinline__ const T* col_wrap(const Sweep2Args<T>& a, int x) {
         if (xw < 0) xw += n;
     }
     return a.src + (long)xw * a.L.col;
+}
+// column x of the walk: periodic (lone slab) or a ghost column of the buffer (SLAB)
+template <typename T, bool SLAB>
+__device__ __forceinline__ const T* col_at(const Sweep2Args<T>& a, int x) {
+    return SLAB ? a.src + (long)x * a.L.col : col_wrap(a, x);
 }
 template <typename T, int VS, int MODE>
 __device__ __forceinline__ void ld_rows_buf(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff, T v[VS]) {
@@ -494,37 +460,18 @@ struct BufOfs {
     unsigned plane;         // bytes between planes
 };
 
-// rc: the buffer resources of columns x-1, x, x+1 (lone slab)
+// rc: the buffer resources of columns x-1, x, x+1
 template <typename T, int VS, int MODE, bool SLAB, int K>
 __device__ __forceinline__ void load_raw_periodic(const Sweep2Args<T>& a, int x, int row0, unsigned off, bool bot,
                                                   bool top, Raw<T, VS>& r, const BufOfs& bo,
                                                   const __amdgpu_buffer_rsrc_t (&rc)[3]) {
-    if (!SLAB) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const __amdgpu_buffer_rsrc_t rk = rc[1 - cx(k)];
-            const unsigned so = (unsigned)k * bo.plane;
-            ld_rows_buf<T, VS, MODE>(rk, bo.lane, so, r.v[k]);
-            if (cy(k) == 1) r.e[k] = ld_one_buf<T>(rk, bo.lo, so);
-            if (cy(k) == -1) r.e[k] = ld_one_buf<T>(rk, bo.hi, so);
-        }
-        r.w[0] = r.w[1] = r.w[2] = r.w[3] = (T)0;
-        if (bot) {
-            r.w[0] = col_deep<T, SLAB, K>(a, x, 7)[0];
-            r.w[1] = col_deep<T, SLAB, K>(a, x, 8)[0];
-        }
-        if (top) {
-            r.w[2] = col_deep<T, SLAB, K>(a, x, 5)[a.L.ny - 1];
-            r.w[3] = col_deep<T, SLAB, K>(a, x, 6)[a.L.ny - 1];
-        }
-        return;
-    }
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
-        const T* p = col_deep<T, SLAB, K>(a, x - cx(k), k) + row0;
-        ld_rows<T, VS, MODE>(p, off, r.v[k]);
-        if (cy(k) == 1) r.e[k] = p[-1];
-        if (cy(k) == -1) r.e[k] = p[64 * VS];
+        const __amdgpu_buffer_rsrc_t rk = rc[1 - cx(k)];
+        const unsigned so = (unsigned)k * bo.plane;
+        ld_rows_buf<T, VS, MODE>(rk, bo.lane, so, r.v[k]);
+        if (cy(k) == 1) r.e[k] = ld_one_buf<T>(rk, bo.lo, so);
+        if (cy(k) == -1) r.e[k] = ld_one_buf<T>(rk, bo.hi, so);
     }
     r.w[0] = r.w[1] = r.w[2] = r.w[3] = (T)0;
     if (bot) {
@@ -558,7 +505,7 @@ __device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (
         const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
         if (flux) {  // wave-uniform branch; the lane condition as a select (no exec-mask branch)
             const double t = (double)ux / a.flux_norm;
-            q += (owner && r0 + e < a.L.ny) ? t : 0.;
+            q += (owner && flux_row(a, r0 + e)) ? t : 0.;
         }
 #pragma unroll
         for (int k = 0; k < 9; ++k) out[k][e] = (T)f[k];
@@ -587,7 +534,7 @@ __device__ __forceinline__ void level_from_raw(const Raw<T, VS>& cur, const Swee
         const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
         if (flux) {  // wave-uniform branch; the lane condition as a select (no exec-mask branch)
             const double t = (double)ux / a.flux_norm;
-            q += (owner && r0 + e < a.L.ny) ? t : 0.;
+            q += (owner && flux_row(a, r0 + e)) ? t : 0.;
         }
 #pragma unroll
         for (int k = 0; k < 9; ++k) out[k][e] = (T)f[k];
@@ -622,16 +569,15 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
     // fin: the flux column is one of the sweep's outputs; level l reaches it at step fi + l - 1
     level_from_raw<T, VS>(cur, a, lane, r0, et, walls, fin && i == fi, owner, q, N);
     if (i + 1 < nl1) {
-        if (!SLAB) {  // the resources of the next column triple: one new column
-            if (DX > 0) {
-                rc[0] = rc[1];
-                rc[1] = rc[2];
-                rc[2] = col_rsrc(col_wrap(a, x + 2));
-            } else {
-                rc[2] = rc[1];
-                rc[1] = rc[0];
-                rc[0] = col_rsrc(col_wrap(a, x - 2));
-            }
+        // the resources of the next column triple: one new column
+        if (DX > 0) {
+            rc[0] = rc[1];
+            rc[1] = rc[2];
+            rc[2] = col_rsrc(col_at<T, SLAB>(a, x + 2));
+        } else {
+            rc[2] = rc[1];
+            rc[1] = rc[0];
+            rc[0] = col_rsrc(col_at<T, SLAB>(a, x - 2));
         }
         load_raw_periodic<T, VS, MODE, SLAB, K>(a, x + DX, row0, off, bot, top, cur, bo, rc);
     }
@@ -644,28 +590,9 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
         if (made) level_from_window<T, VS, DX>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, owner, q, out);
         // level K's columns of the made steps are exactly the sweep's outputs [xa, xb)
         if (made && l == K && owner) {
-            if (!SLAB) {
-                const __amdgpu_buffer_rsrc_t rd = col_rsrc<T>(a.dst + (long)c * a.L.col);
+            const __amdgpu_buffer_rsrc_t rd = col_rsrc<T>(a.dst + (long)c * a.L.col);
 #pragma unroll
-                for (int k = 0; k < 9; ++k) st_rows_buf<T, VS, MODE>(rd, bo.lane, (unsigned)k * bo.plane, out[k]);
-            } else {
-                T* dst = a.dst + (long)c * a.L.col + row0;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) st_rows<T, VS, MODE>(dst + (long)k * a.L.plane, off, out[k]);
-            }
-            // slab of a group: the output columns within K of an edge are the deep halo the
-            // neighbour needs next cycle (wave-uniform: c is the walk's column); written here
-            // instead of by a pack kernel after the sweep
-            if (SLAB && a.send_left && (c < K || c >= a.L.ncol - K)) {
-                const bool to_left = c < K;
-                const int d = to_left ? c : a.L.ncol - 1 - c;
-                T* sb = (to_left ? a.send_left : a.send_right) + row0;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    const int slot = deep_slot(!to_left, d, k, K);
-                    if (slot >= 0) st_rows<T, VS, 0>(sb + (long)slot * a.L.rows, off, out[k]);
-                }
-            }
+            for (int k = 0; k < 9; ++k) st_rows_buf<T, VS, MODE>(rd, bo.lane, (unsigned)k * bo.plane, out[k]);
         }
         copy_col<T, VS>(WA[l - 2], WB[l - 2]);
         copy_col<T, VS>(WB[l - 2], N);
@@ -698,11 +625,9 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
     bo.plane = (unsigned)(a.L.plane * (long)sizeof(T));
     Raw<T, VS> cur;
     __amdgpu_buffer_rsrc_t rc[3];
-    if (!SLAB) {
-        rc[0] = col_rsrc(col_wrap(a, x0 - 1));
-        rc[1] = col_rsrc(col_wrap(a, x0));
-        rc[2] = col_rsrc(col_wrap(a, x0 + 1));
-    }
+    rc[0] = col_rsrc(col_at<T, SLAB>(a, x0 - 1));
+    rc[1] = col_rsrc(col_at<T, SLAB>(a, x0));
+    rc[2] = col_rsrc(col_at<T, SLAB>(a, x0 + 1));
     load_raw_periodic<T, VS, MODE, SLAB, K>(a, x0, row0, off, bot, top, cur, bo, rc);
     const bool fin = a.flux_col >= xa && a.flux_col < xb;
     const int fi = REV ? xb + K - 2 - a.flux_col : a.flux_col - xa + K - 1;  // step of level 1 at the flux column
@@ -714,15 +639,14 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
     return q;
 }
 
-// wave -> (sweep, chunk) of the linear order, optionally dealt to the XCDs in contiguous ranges
-// (xcds: the XCDs the launch's workgroups are dealt over, 0 = 8; the dispatcher deals over all
-// eight whatever the stream's CU mask, profiles/r02n_xcc_probe.txt)
-__device__ __forceinline__ void linear_item(int map, int nch, int xcds, int wv, int& sw, int& ch) {
+// wave -> (sweep, chunk) of the linear order, optionally (map 2) dealt to the eight XCDs in
+// contiguous ranges (the dispatcher deals workgroups round-robin over all eight whatever the
+// stream's CU mask, profiles/r02n_xcc_probe.txt)
+__device__ __forceinline__ void linear_item(int map, int nch, int wv, int& sw, int& ch) {
     int b = (int)blockIdx.x;
     if (map == 2) {
-        const int nx = xcds > 0 ? xcds : 8;
-        const int q = (int)gridDim.x / nx;
-        if (b < nx * q) b = (b % nx) * q + b / nx;
+        const int q = (int)gridDim.x / 8;
+        if (b < 8 * q) b = (b % 8) * q + b / 8;
     }
     const int gw = b * 4 + wv;
     sw = gw / nch;
@@ -740,18 +664,10 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int sw, ch;
-    linear_item(a.map, a.nch, a.xcds, wv, sw, ch);
+    linear_item(a.map, a.nch, wv, sw, ch);
     if (sw >= a.nsweep || ch >= a.nch) return;
     int xa, xb;
-    if (a.sweep_tab && a.tab_rows) {
-        const int* e = a.sweep_tab + 4 * sw;
-        if (ch < e[2] || ch >= e[3]) return;  // wave-uniform: rows of an IB patch
-        xa = __builtin_amdgcn_readfirstlane(e[0]);
-        xb = __builtin_amdgcn_readfirstlane(e[1]);
-    } else if (a.sweep_tab) {
-        xa = __builtin_amdgcn_readfirstlane(a.sweep_tab[2 * sw]);
-        xb = __builtin_amdgcn_readfirstlane(a.sweep_tab[2 * sw + 1]);
-    } else if (a.col_step > 0) {
+    if (a.col_step > 0) {
         xa = a.col_begin + sw * a.col_step;
         xb = min(xa + a.W, a.col_end);
     } else {  // balanced: nsweep sweeps of floor/ceil((col_end - col_begin) / nsweep) columns
@@ -804,7 +720,7 @@ static long resident_waves(int cus) {
 
 template <typename T, int VS, int MODE, int K, bool SLAB>
 static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s) {
-    if (b.col_step <= 0 && !b.sweep_tab) {
+    if (b.col_step <= 0) {
         // balanced sweeps: the wave count a whole number of device-wide rounds (the waves of one
         // launch all do the same work, so a partial last round idles the chip), sweeps close to
         // the requested W columns

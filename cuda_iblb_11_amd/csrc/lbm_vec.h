@@ -76,19 +76,9 @@ __device__ __forceinline__ float lane_shift(float v) {
     return __int_as_float(dpp_shift<DIR>(__float_as_int(v)));
 }
 
-// An element offset the compiler must treat as per-lane (VE = true): the load through it becomes a
-// vector load.  A wave-uniform address is otherwise loaded through the scalar data cache, which a
-// kernel that reads what it wrote itself after a workgroup barrier (band_kernel) would see stale:
-// the agent-scope acquire invalidates the vector L1 only.
-template <bool VE>
-__device__ __forceinline__ long vofs(long o) {
-    if (VE) asm volatile("" : "+v"(o));
-    return o;
-}
-
 // Rows y0-1 .. y0+V-2 (DIR = +1, planes with c_y = +1) or y0+1 .. y0+V (DIR = -1) of plane
 // pointer p (column base), for a wave covering rows [cs, cs + 64V).
-template <typename T, int V, int MODE, int DIR, bool VE = false>
+template <typename T, int V, int MODE, int DIR>
 __device__ __forceinline__ typename VT<T, V>::type ld_shifted(const T* p, int y0, int cs, int lane) {
     typedef typename VT<T, V>::type vec;
     if (!(MODE & MODE_SHIFT)) return ldu<T, V>(p + y0 - DIR);
@@ -97,14 +87,14 @@ __device__ __forceinline__ typename VT<T, V>::type ld_shifted(const T* p, int y0
     if (DIR > 0) {
         // element 0 = last element of the previous lane; lane 0: row cs-1 (scalar load)
         T prev = lane_shift<+1>(a[V - 1]);
-        const T edge = p[vofs<VE>(cs - 1)];
+        const T edge = p[cs - 1];
         if (lane == 0) prev = edge;
         r[0] = prev;
 #pragma unroll
         for (int e = 1; e < V; ++e) r[e] = a[e - 1];
     } else {
         T next = lane_shift<-1>(a[0]);
-        const T edge = p[vofs<VE>(cs + 64 * V)];
+        const T edge = p[cs + 64 * V];
         if (lane == 63) next = edge;
 #pragma unroll
         for (int e = 0; e < V - 1; ++e) r[e] = a[e + 1];

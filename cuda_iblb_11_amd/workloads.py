@@ -65,16 +65,20 @@ def filament(it: int, n_points: int = 256, x0: float = 1024.0, y0: float = 1.0, 
 
 
 def filament_array(it: int, nx: int, n_fil: int = 64, pts: int = 96, dy: float = 1.0, U0: float = 1e-3,
-                   period: int = 1000):
+                   period: int = 1000, x_offset: float = 0.5):
     """Array of n_fil prescribed filaments evenly spaced in x with a metachronal phase lag
-    (config K5 stand-in for the reference's cilia; 64 x 96 = 6144 points)."""
+    (config K5 stand-in for the reference's cilia; 64 x 96 = 6144 points).  Filament m stands at
+    x = (m + x_offset) * nx / n_fil and tilts by up to 8 columns; x_offset = 0 (config K5 as
+    BASELINE.json states it, "filaments spanning slab boundaries") puts one on every edge of an
+    x-slab decomposition into 1, 2, 4 or 8 slabs (x = 0 included), and positions are wrapped into
+    [0, XDIM) like the reference's boundary_check (main.cu:193-196)."""
     s_all, u_all = [], []
     space = nx / n_fil
     for m in range(n_fil):
         k = np.arange(pts, dtype=np.float64)
         ph = 2.0 * np.pi * (it + m * period / n_fil) / period
         tilt = (k / pts) ** 2 * 8.0 * np.sin(ph)
-        xs = (m + 0.5) * space + tilt
+        xs = np.mod((m + x_offset) * space + tilt, nx)
         ys = 1.0 + dy * k
         s = np.empty(2 * pts)
         s[0::2], s[1::2] = xs, ys

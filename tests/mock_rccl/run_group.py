@@ -4,7 +4,7 @@ iblb_step / readers) with N ranks as threads on one GPU, through the mock-RCCL b
 (tests/mock_rccl/libiblb_mockrccl.so), and compare with a single-slab context of the same
 build.  Prints one JSON line; exit status 0 = match.
 
-usage: run_group.py NRANKS NX NY STEPS WITH_IB(0/1) PRECISION(f64/f32) [BULK(0/1)]
+usage: run_group.py NRANKS NX NY STEPS WITH_IB(0/1/2/3) PRECISION(f64/f32) [BULK(0/1)]
 
 BULK=1 (no IB): the group advances in multi-step calls (two-iteration sweeps with the 2-step
 halo, one-step launches for odd remainders) instead of one iteration per call.
@@ -27,10 +27,13 @@ from cuda_iblb_11_amd.lattice import Lattice, plan_slabs, rccl_unique_id, split_
 
 def main():
     n, nx, ny, steps, with_ib, prec = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]),
-                                        sys.argv[5] in ("1", "2"), sys.argv[6])
+                                        sys.argv[5] in ("1", "2", "3"), sys.argv[6])
     # IB mode "2": one filament moving inside each slab, points given ahead (iblb_set_lagrangian_steps)
-    # and stepped in bulk: the IB band cycle of slab groups
-    band = sys.argv[5] == "2"
+    # and stepped in bulk: the IB band cycle of slab groups.  Mode "3": one moving filament across
+    # EVERY slab edge (x = 0 included, wrapped into [0, XDIM) like boundary_check, main.cu:193-196):
+    # the band cycle with ghost-column trapezoids on every rank, also checked against the oracle
+    band = sys.argv[5] in ("2", "3")
+    straddle = sys.argv[5] == "3"
     bulk = len(sys.argv) > 7 and sys.argv[7] == "1" and (not with_ib or band)
     lib = L.load_from(os.path.join(HERE, "libiblb_mockrccl.so"))
     rho, u = W.perturbed_state(nx, ny, 31)
@@ -54,11 +57,23 @@ def main():
                                         period=20, sway=0.8))
             return tuple(np.concatenate(q) for q in zip(*parts))
 
+    if straddle:
+        def pts(it):
+            parts = []
+            for r, (xb_, xc_) in enumerate(plan_slabs(nx, n)):
+                ph = 2 * np.pi * (it + 3 * r) / 20
+                f = W.filament(it, n_points=12, x0=xb_ + 0.3 + 1.5 * np.sin(ph), y0=10.0 + 7 * r, U0=2e-3,
+                               period=20, sway=1.2)
+                f[0][0::2] = np.mod(f[0][0::2], nx)  # wrapped into [0, XDIM)
+                parts.append(f)
+            return tuple(np.concatenate(q) for q in zip(*parts))
+
     def sched(t0, k):
         e = [pts(it) for it in range(t0, t0 + k)]
         return np.stack([x[0] for x in e]), np.stack([x[1] for x in e]), np.stack([x[2] for x in e])
 
-    single = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, lib=lib)
+    fcol = int(os.environ.get("RUN_GROUP_FLUX_COLUMN", nx - 5))  # (diagnostics: another flux column)
+    single = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, lib=lib, flux_column=fcol)
     single.set_state(rho, u)
     for it in range(steps):
         if with_ib:
@@ -68,6 +83,21 @@ def main():
     r1, u1 = single.macro()
     q1 = single.flux
     f1 = single.lagrangian_force() if with_ib else None
+    d_oracle = None
+    if straddle:  # the restatement of the reference, one iteration at a time
+        from oracle import oracle as O
+        O.load()
+        sim = O.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=bf, flux_column=fcol)
+        for it in range(steps):
+            sim.set_lagrangian(*pts(it))
+            sim.step(1)
+        ro, uo = np.asarray(sim.rho).copy(), np.asarray(sim.u).copy()
+
+    def vs_oracle(rr, uu):  # each field normalised by its own max (rho - 1, not rho ~ 1)
+        N = nx * ny
+        return {"rho-1": float(np.max(np.abs((rr - 1) - (ro - 1))) / np.max(np.abs(ro - 1))),
+                "ux": float(np.max(np.abs(uu[:N] - uo[:N])) / np.max(np.abs(uo[:N]))),
+                "uy": float(np.max(np.abs(uu[N:] - uo[N:])) / np.max(np.abs(uo[N:])))}
 
     uid = rccl_unique_id(lib)
     out = [None] * n
@@ -92,7 +122,7 @@ def main():
     def worker(r):
         xb, xc = plan_slabs(nx, n)[r]
         lat = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, x_begin=xb,
-                      x_count=xc, lib=lib)
+                      x_count=xc, lib=lib, flux_column=fcol)
         lat.set_state(split_state(rho, 1, nx, ny, xb, xc), split_state(u, 2, nx, ny, xb, xc))
         lat.attach_rccl(uid, n, r)
         if band:
@@ -114,7 +144,7 @@ def main():
                 lat.set_lagrangian(*pts(it))
             lat.step(1)
         if band and lat.timing()["sweepk_launches"] == 0:
-            raise RuntimeError("the band cycle did not run")
+            raise RuntimeError(f"rank {r}: the band cycle did not run")
         rs, us = lat.macro()
         out[r] = (xb, xc, rs, us, lat.flux, lat.lagrangian_force() if with_ib else None)  # collective
         gathered[r] = lat.gather_macro(0)  # collective output gather to rank 0
@@ -126,7 +156,7 @@ def main():
     def resume(r):  # fresh contexts: attach, restore the mid-run checkpoint, finish the run
         xb, xc = plan_slabs(nx, n)[r]
         lat = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, x_begin=xb,
-                      x_count=xc, lib=lib)
+                      x_count=xc, lib=lib, flux_column=fcol)
         lat.attach_rccl(uid2, n, r)
         lat.load_checkpoint(ck(r))
         if band:  # the checkpoint holds the points of iteration half-1; the rest given ahead again
@@ -179,9 +209,14 @@ def main():
     if with_ib:  # every rank reports the whole F_s (summed over the slabs that hold it)
         d_fs = max(float(np.max(np.abs(o[5] - f1)) / np.max(np.abs(f1))) for o in out)
         ok = ok and d_fs <= 1e-5
+    if straddle:  # the group (band cycles across every slab edge) against the restatement
+        d_oracle = vs_oracle(R, U)
+        d_oracle["flux"] = float(abs(fluxes[0] - sim.flux) / max(abs(sim.flux), 1e-300))
+        d_oracle["flux_single"] = float(abs(q1 - sim.flux) / max(abs(sim.flux), 1e-300))
+        ok = ok and max(d_oracle.values()) <= (1e-9 if prec == "f64" else 1e-4)
     print(json.dumps({"ok": bool(ok), "exact": exact, "d_rho": d_rho, "d_u": d_u, "d_flux": d_q, "n": n,
                       "gather_ok": g_ok, "restart_ok": bool(rs_ok), "d_restart": d_re, "d_F_s": d_fs,
-                      "with_ib": with_ib, "precision": prec}), flush=True)
+                      "with_ib": with_ib, "precision": prec, "d_oracle": d_oracle}), flush=True)
     sys.exit(0 if ok else 1)
 
 

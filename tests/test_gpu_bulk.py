@@ -216,13 +216,15 @@ def test_k3_time_varying_filament(gpu, oracle, threads):
 
 def test_k5_filament_array_f32(gpu, oracle, threads):
     """K5 on one GPU: 8192 x 2048 f32 + 64 filaments x 96 points (6144) that move every
-    iteration (W.filament_array(it)), 11 iterations in one call: boot + two band cycles."""
+    iteration, one on every slab edge of an 8-slab split (x = 0 included, the filament there
+    crosses it: ghost-column trapezoids), 11 iterations in one call: boot + two band cycles;
+    rho - 1 and u each normalised by its own max."""
     from cuda_iblb_11_amd import workloads as W
-    pts = lambda it: W.filament_array(it, 8192, n_fil=64, pts=96, period=200)
+    pts = lambda it: W.filament_array(it, 8192, n_fil=64, pts=96, period=200, x_offset=0.0)
     lat, sim = moving_run(gpu, oracle, 8192, 2048, pts, [11], precision="f32", body_force=W.BODY_FORCE)
     assert lat.timing()["sweepk_launches"] == 2
     r = fields(lat, sim)
-    assert max(r["rho"], r["ux"], r["uy"]) <= TOL32, r
+    assert max(r["rho-1"], r["ux"], r["uy"]) <= TOL32, r
 
 
 def test_band_streams_keep_the_context_stream(gpu, monkeypatch):
@@ -264,18 +266,16 @@ def test_band_streams_keep_the_context_stream(gpu, monkeypatch):
     assert rel(r1, r2) <= 1e-13 and rel(u1, u2) <= 1e-12
 
 
-@pytest.mark.parametrize("precision,fused", [("f64", 1), ("f32", 1), ("f64", 0)])
-def test_rccl_self_ring_ib_band_cycle(gpu, monkeypatch, precision, fused):
+@pytest.mark.parametrize("precision,where", [("f64", "inside"), ("f32", "inside"), ("f64", "edge"), ("f32", "edge")])
+def test_rccl_self_ring_ib_band_cycle(gpu, monkeypatch, precision, where):
     """The IB band cycle of a slab group over REAL RCCL (one rank, its own neighbour): moving
-    filaments inside the slab, points given ahead, bulk calls with readers between them; equals
-    the lone slab (same band cycle without halos) up to the spread atomics' order.  fused: the
-    band chain as one launch on its own CU-masked stream beside the deep sweep (default), or the
-    2K-launch chain on the compute stream."""
+    filaments, points given ahead, bulk calls with readers between them; equals the lone slab up to
+    the spread atomics' order.  inside: the filaments stay inside the slab; edge: they cross the
+    slab edge (x = 0): the cycle's exchange carries 3K ghost columns and the trapezoids advance them."""
     from cuda_iblb_11_amd import workloads as W
     monkeypatch.setenv("IBLB_RCCL_SELF", "1")
-    monkeypatch.setenv("IBLB_BAND_FUSED", str(fused))
     nx, ny = 256, 128
-    pts = _swaying(nx, n_fil=2, pts=40)
+    pts = _swaying(nx, n_fil=2, pts=40) if where == "inside" else _crossing(nx)
     rho, u = W.perturbed_state(nx, ny, 17)
     kw = dict(precision=precision, body_force=(1e-6, 0.0), max_points=80)
     ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)
@@ -297,3 +297,36 @@ def test_rccl_self_ring_ib_band_cycle(gpu, monkeypatch, precision, fused):
     assert ring.timing()["sweepk_launches"] >= 4
     assert abs(ring.flux - ref.flux) <= 1e-11 * abs(ref.flux)
     ring.close()
+
+
+def _crossing(nx, pts=40, period=24):
+    """Two filaments that sway across x = 0 / XDIM (wrapped into [0, XDIM) like boundary_check,
+    main.cu:193-196) and one near XDIM-1."""
+    def points(it):
+        k = np.arange(pts)
+        s_all, u_all = [], []
+        for m, (x0, y0) in enumerate(((0.3, 2.0), (nx - 2.2, 50.0))):
+            ph = 2 * np.pi * (it + 5 * m) / period
+            s = np.empty(2 * pts, np.float32)
+            s[0::2] = np.mod(x0 + 2.0 * (k / pts) * np.sin(ph), nx)
+            s[1::2] = y0 + k
+            us = np.zeros(2 * pts, np.float32)
+            us[0::2] = 2e-3 * (k / pts) * np.cos(ph)
+            s_all.append(s)
+            u_all.append(us)
+        s = np.concatenate(s_all)
+        return s, np.concatenate(u_all), np.ones(s.size // 2, np.int32)
+    return points
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_moving_points_across_x0(gpu, oracle, precision, monkeypatch):
+    """Filaments swaying across x = 0 through the lone slab's band cycle (ghost columns filled by
+    periodic copies every cycle), against the oracle."""
+    nx, ny = 256, 128
+    lat, sim = moving_run(gpu, oracle, nx, ny, _crossing(nx), [1, 12, 5, 3, 15], precision=precision,
+                          monkeypatch=monkeypatch, readers=True)
+    assert lat.timing()["sweepk_launches"] >= 6
+    r = fields(lat, sim)
+    assert max(r["rho-1"], r["ux"], r["uy"]) <= (1e-10 if precision == "f64" else TOL32), r
+    assert abs(lat.flux - sim.flux) <= (1e-9 if precision == "f64" else 1e-4) * max(abs(sim.flux), 1e-30)
