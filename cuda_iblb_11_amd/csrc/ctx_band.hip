@@ -28,6 +28,7 @@
 // columns per level (a force's nodes reach 2, their pulls 3), so after K levels it stops short of
 // the slab's own columns when gc >= 3K.  Only the slab's own columns are stored.
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 
 #include "ctx.h"
@@ -257,6 +258,13 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     c->band_d = bd;
     c->band_x = bx;
     c->band_valid = true;
+    if (env_long("IBLB_DEBUG_PLAN", 0)) {
+        std::fprintf(stderr, "[iblb plan] x_begin %d t %lld: %zu patches", c->x_begin, c->t, b.size());
+        for (auto& p : b) std::fprintf(stderr, " [%d,%d]x[%d,%d]", p[0], p[1], p[2], p[3]);
+        std::fprintf(stderr, " d %d x %d flux %d rows [%d,%d) entries", bd, bx, c->band_flux, c->band_fy0, c->band_fy1);
+        for (int j = 0; j < K; ++j) std::fprintf(stderr, " %d", cnt[j]);
+        std::fprintf(stderr, "\n");
+    }
     return IBLB_OK;
 }
 

@@ -29,7 +29,7 @@ struct FusedArgs {
                         // (columns -gc .. ncol+gc-1 addressable: the pointer is at column 0)
     double* fdense;     // dense IB force, x plane then y plane (column stride rows; column 0)
     long fplane;
-    int flux_col;       // local column sampled for Q, or -1
+    int flux_col;       // local column sampled for Q (>= 0), or -1 (none: never column -1, a ghost column)
     double flux_norm;
     double* Q;
     Coef c;

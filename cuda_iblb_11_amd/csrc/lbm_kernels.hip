@@ -95,7 +95,7 @@ __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, 
         if (lane == 0) a.flags[(long)xc * a.nch + ch] = 0;  // only this wave reads this flag
     }
 
-    const bool do_flux = xc == a.flux_col;
+    const bool do_flux = a.flux_col >= 0 && xc == a.flux_col;  // (-1: none; ghost column -1 is a real column)
     double q = 0.;
 #pragma unroll
     for (int e = 0; e < V; ++e) {

@@ -629,7 +629,7 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
     rc[1] = col_rsrc(col_at<T, SLAB>(a, x0));
     rc[2] = col_rsrc(col_at<T, SLAB>(a, x0 + 1));
     load_raw_periodic<T, VS, MODE, SLAB, K>(a, x0, row0, off, bot, top, cur, bo, rc);
-    const bool fin = a.flux_col >= xa && a.flux_col < xb;
+    const bool fin = a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb;
     const int fi = REV ? xb + K - 2 - a.flux_col : a.flux_col - xa + K - 1;  // step of level 1 at the flux column
     // (a main loop without the per-level `made` checks, after 2(K-1) window-filling iterations,
     // lets the compiler hoist the collide constants into registers: VGPR spills, 512 VGPRs)
@@ -691,7 +691,7 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
                      : sweepk_walk<T, VS, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top))
               : (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
                      : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top));
-    if (a.flux_col >= xa && a.flux_col < xb) {
+    if (a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb) {
         const double qs = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, qs);
     }

@@ -75,10 +75,14 @@ def main():
     fcol = int(os.environ.get("RUN_GROUP_FLUX_COLUMN", nx - 5))  # (diagnostics: another flux column)
     single = Lattice(nx, ny, W.TAU, W.TAU2, precision=prec, body_force=bf, max_points=mp, lib=lib, flux_column=fcol)
     single.set_state(rho, u)
+    trace = os.environ.get("RUN_GROUP_TRACE") == "1"  # diagnostics: flux after every call
+    q_single = {}
     for it in range(steps):
         if with_ib:
             single.set_lagrangian(*pts(it))
         single.step(1)
+        if trace:
+            q_single[it + 1] = single.flux
     # (mode 2: the reference run takes the points per iteration, the slabs get them ahead)
     r1, u1 = single.macro()
     q1 = single.flux
@@ -134,9 +138,25 @@ def main():
                 if t + k <= half:
                     lat.step(k)
                     t += k
+                    if trace:
+                        q = lat.flux
+                        if r == 0:
+                            print("trace", t, q, q_single[t], flush=True)
             lat.step(half - t)
+            if trace:
+                q = lat.flux
+                if r == 0:
+                    print("trace", half, q, q_single[half], flush=True)
             lat.save_checkpoint(ck(r))
-            lat.step(steps - half)
+            if trace:
+                for k in ([5, 5, 3] if steps - half == 13 else [steps - half]):
+                    lat.step(k)
+                    t2 = lat.steps
+                    q = lat.flux
+                    if r == 0:
+                        print("trace", t2, q, q_single[t2], flush=True)
+            else:
+                lat.step(steps - half)
         for it in range(0 if not bulk else steps, steps):
             if it == half:
                 lat.save_checkpoint(ck(r))
