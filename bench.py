@@ -47,7 +47,7 @@ WORKLOADS = {
 }
 
 
-def workload_points(kind, nx):
+def workload_points(kind, nx, offset=0.0):
     """Lagrangian points of iteration `it` (a function), IB evaluated every iteration:
     K3: one 256-point filament at x = nx/2, u_s = (U0 (k/255) sin(2 pi it/T), 0)
     changing every iteration; K5: 64 filaments x 96 points (W.filament_array) whose points move
@@ -58,7 +58,7 @@ def workload_points(kind, nx):
         return lambda it: W.filament(it, n_points=256, x0=nx / 2 + 0.3, y0=1.0, dy=1.0, U0=1e-3, period=1000)
     if kind == "array":  # 64 filaments per 8192 columns, one on every slab edge (BASELINE config 5)
         nf = max(1, round(64 * nx / 8192))
-        return lambda it: W.filament_array(it, nx, n_fil=nf, pts=96, period=1000, x_offset=0.0)
+        return lambda it: W.filament_array(it, nx, n_fil=nf, pts=96, period=1000, x_offset=offset)
     return None
 
 
@@ -105,6 +105,9 @@ def parse():
                         "clock settles under load; reported as `prime` in the JSON line)")
     p.add_argument("--frozen", action="store_true",
                    help="IB workloads: points of iteration 250 for the whole run (round-1 workload)")
+    p.add_argument("--filament-offset", type=float, default=0.0,
+                   help="K5: filament m stands at (m + offset) * 128 columns (0 = on every slab edge, the BASELINE "
+                        "config; 0.5 = the round-2 layout, every filament mid-slab)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU sample duration")
     p.add_argument("--no-profile-events", action="store_true", help="skip per-launch HIP events")
@@ -264,7 +267,7 @@ def main():
     # 8 filaments per 1024 columns, one on the slab edge).
     rehearsal = distributed and a.same_device
     lnx = xc if rehearsal else nx
-    points = workload_points(wpts, lnx)
+    points = workload_points(wpts, lnx, a.filament_offset)
     ns = 0 if points is None else points(0)[0].size // 2
     lat = P.Lattice(lnx, ny, W.TAU, W.TAU2, precision=precision, body_force=W.BODY_FORCE, device=local,
                     x_begin=0 if rehearsal else xb, x_count=xc if world > 1 and not rehearsal else 0, max_points=ns)

@@ -134,14 +134,15 @@ struct iblb_ctx {
     std::vector<int> band_off, band_n, band_nchl;  // level j: first entry, entries, chunks per entry
     long long band_deep_lu = 0, band_lu = 0;       // cells of the deep sweep / of all trapezoid levels
     int band_flux = -1, band_fy0 = 0, band_fy1 = 0;  // flux column in a patch output, the patch's rows
-    bool band_edge_prev = false; // the last cycle's trapezoids wrote the slab's edge columns
+    bool band_run = false;       // the last step was a band cycle on band_st / deep_st (not joined)
+    hipEvent_t band_end = nullptr; // recorded on the deep stream at the end of the last band cycle
     char* s_alloc = nullptr;     // two scratch population buffers of the trapezoid (layout of g)
     void* sbuf[2] = {nullptr, nullptr};
-    int band_reserve = 0;        // CUs of the band chain's stream (0: one stream, in sequence)
+    int band_reserve = 0;        // CUs of the band chain's stream (0: one stream, in sequence; -2: unmasked)
     bool band_sticky = false;    // keep the streams while a schedule runs
     hipStream_t band_st = nullptr;  // the band chain (masked to the reserved CUs)
     hipStream_t deep_st = nullptr;  // the cycle's deep sweep (masked to the other CUs)
-    hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_b2 = nullptr, ev_bd = nullptr;
+    hipEvent_t ev_b0 = nullptr, ev_bd = nullptr;
     // flux: d_Q[0] cumulative, d_Q[1] scratch
     double* d_Q = nullptr;
     // state machine
@@ -298,6 +299,7 @@ bool band_ready(const iblb_ctx* c);
 int band_step_any(iblb_ctx* c);
 int plan_bands(iblb_ctx* c, const std::vector<float>& xy);
 int plan_cycle(iblb_ctx* c);
+int band_join(iblb_ctx* c);     // the context's stream after a run of band cycles
 int band_release(iblb_ctx* c);  // streams, events, pinned tables, scratch buffers
 
 }  // namespace iblbh

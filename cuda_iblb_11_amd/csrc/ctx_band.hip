@@ -54,10 +54,15 @@ bool band_ready(const iblb_ctx* c) {
 // others.  A lone slab may use the whole chip; a slab of an RCCL group the compute stream's CUs
 // (the comm stream keeps its reserved CUs for the exchange and the boundary sweeps).  The context's
 // stream is never replaced: both start after it and it waits for both.  The chain (2K dependent
-// small launches, latency-bound) gets one XCD's worth of CUs, two where the trapezoids hold more
-// than 5 % of the cycle's lattice updates.
+// small launches, latency-bound: ~8 us each uncontended) gets one XCD's worth of CUs, two where the
+// trapezoids hold more than 5 % of the cycle's lattice updates.  A lone slab whose deep sweep runs
+// for at least 1.5x that chain (>= 4M cells a level at K = 5, 2048^2 and up) instead leaves both
+// streams unmasked with the chain's at the highest priority: the chain has the slack to wait for CUs
+// the deep sweep's workgroups free, and the deep sweep gets the whole chip (profiles/r03ch: K3 +5 %,
+// K5 +5 %; the K5-width slab 1024 x 2048, whose chain is as long as its deep sweep, -4 to -9 %).
 static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
     const bool slab = rccl_multi(c);
+    int rc_;
     if (c->transport == TR_LOCAL) return IBLB_OK;
     if (!c->ncu) {
         hipDeviceProp_t prop;
@@ -67,6 +72,8 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
     const int per_xcd = std::max(1, c->ncu / 8);
     const double share = (double)band_cols / (double)std::max(1LL, band_cols + (long long)c->sweep_depth * deep_cols);
     long want = (share > 0.05 ? 2 : 1) * per_xcd;
+    const double deep_us = (double)c->sweep_depth * deep_cols * c->ny / (is_f64(c) ? 130e3 : 190e3);
+    if (!slab && deep_us >= 1.5 * 2 * c->sweep_depth * 8.0) want = -2;
     std::vector<uint32_t> base((size_t)(c->ncu + 31) / 32, 0u);
     int avail = 0;
     for (int i = 0; i < c->ncu; ++i)
@@ -74,8 +81,13 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
             base[(size_t)i / 32] |= 1u << (i % 32);
             ++avail;
         }
+    // IBLB_BAND_CUS: CUs of the chain's stream; -2: both streams unmasked, the chain's at the highest
+    // priority; 0: one stream, the chain and the deep sweep in sequence
+    want = env_long("IBLB_BAND_CUS", want);
+    if (want == -2 && slab) want = per_xcd;  // a group slab's comm stream owns the reserved CUs
     if (want >= avail) want = 0;
     if (want == c->band_reserve || (c->band_sticky && c->band_st)) return IBLB_OK;
+    if ((rc_ = band_join(c))) return rc_;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     for (hipStream_t* st : {&c->band_st, &c->deep_st})
         if (*st) {
@@ -83,7 +95,12 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
             (void)hipStreamDestroy(*st);
             *st = nullptr;
         }
-    if (want) {
+    if (want == -2) {
+        int lo = 0, hi = 0;
+        HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(c, hipStreamCreateWithPriority(&c->band_st, hipStreamNonBlocking, hi));
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->deep_st, hipStreamNonBlocking));
+    } else if (want > 0) {
         std::vector<uint32_t> deep(base.size(), 0u), band(base.size(), 0u);
         long taken = 0;
         for (int i = c->ncu - 1; i >= 0; --i) {
@@ -95,7 +112,7 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
         HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->deep_st, (uint32_t)deep.size(), deep.data()));
         HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->band_st, (uint32_t)band.size(), band.data()));
     }
-    for (hipEvent_t* e : {&c->ev_b0, &c->ev_b1, &c->ev_b2, &c->ev_bd})
+    for (hipEvent_t* e : {&c->ev_b0, &c->ev_bd})
         if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventDisableSystemFence));
     c->band_reserve = (int)want;
     return IBLB_OK;
@@ -213,7 +230,8 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     // the tables go to a ring of pinned (device-visible, coherent) host slots that the cycle's
     // launches read directly: a new plan of moving points costs no copy on the cycle's critical
     // path; a slot is rewritten only after the event of the last cycle that read it
-    if (tab.size() > c->band_pin_cap) {
+    if (tab.size() > c->band_pin_cap) {  // every slot may be in use: wait for the cycles in flight
+        if ((rc = band_join(c))) return rc;
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         const size_t cap = std::max(tab.size(), (size_t)5 * (K + 1) * (ncol + 2 * D) + 64);
         for (int i = 0; i < BAND_PIN_SLOTS; ++i) {
@@ -307,7 +325,7 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     Sweep2Args<T> d = sweep_args<T>(c, lo, c->deep_balance ? 0 : W, hi, (n + W - 1) / W, W);
     d.vs = slab ? c->slab_vs : c->deep_vs;
     d.variant = c->deep_variant;
-    d.cus = c->ncu ? (slab ? c->ncu - c->reserved_cus : c->ncu) - c->band_reserve : 0;
+    d.cus = c->ncu ? (slab ? c->ncu - c->reserved_cus : c->ncu) - std::max(0, c->band_reserve) : 0;
     if (c->band_flux >= 0) {
         d.fskip0 = c->band_fy0;
         d.fskip1 = c->band_fy1;
@@ -397,14 +415,18 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
     return IBLB_OK;
 }
 
-// One band cycle.  A lone slab: the chain and the deep sweep on two masked streams beside each
-// other (D > 0: the chain first fills the ghost columns with periodic copies).  A slab of an RCCL
-// group additionally:
-//   comm:    [after the last cycle if it stored edge columns or the halo is deeper than K]
-//            exchange(t, band_x columns) -> [ev_x] -> wait ev_pre (the last cycle read the columns
+// One band cycle.  A lone slab: the chain (on bs) beside the deep sweep (on ds; D > 0: the chain
+// first fills the ghost columns with periodic copies), the last level on ds right behind the deep
+// sweep.  Consecutive cycles stay on the two streams: the next deep sweep follows the last level
+// on ds in stream order and the next chain waits for it (band_end), so a cycle costs two cross-queue
+// waits (K3 timeline, profiles/r03k: joining both streams into the context's stream and starting
+// the next cycle from there left 30-40 us of idle chip per cycle); band_join joins them when the
+// run of cycles ends.  A slab of an RCCL group additionally:
+//   comm:    [after the last cycle when it stored edge columns or the halo is deeper than K]
+//            exchange(t, band_x columns) -> [ev_x] -> after the last cycle (it read the columns
 //            the boundary sweeps overwrite) -> boundary sweeps [0, K), [ncol-K, ncol) -> ev_bnd
-//   compute: the deep sweep of the interior beside the band chain (which waits for ev_x when its
-//            trapezoids read ghosts, and stores its edge columns after ev_bnd)
+//   ds, bs:  after boundary(t-K) (they read its columns); the chain waits for ev_x when its
+//            trapezoids read ghosts and its last level stores edge columns after ev_bnd
 template <typename T>
 static int band_step(iblb_ctx* c) {
     const int K = c->sweep_depth, D = c->band_d;
@@ -415,14 +437,31 @@ static int band_step(iblb_ctx* c) {
     const bool slab = !single_slab(c);
     const bool ov = c->band_st != nullptr;
     hipStream_t bs = ov ? c->band_st : c->stream, ds = ov ? c->deep_st : c->stream;
+    const bool chained = ov && c->band_run;  // the previous step was a band cycle on these streams
+    if (!chained) {
+        if ((rc = join_comm(c))) return rc;
+        if (slab) HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
+        if (ov) {
+            HIP_TRY(c, hipEventRecord(c->ev_b0, c->stream));
+            HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_b0, 0));
+            HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_b0, 0));
+        }
+    } else {
+        HIP_TRY(c, hipStreamWaitEvent(bs, c->band_end, 0));  // g^t complete: the last level of t-K on ds
+        if (slab) {  // boundary(t-K) wrote columns both read
+            HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_bnd, 0));
+            HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_bnd, 0));
+        }
+    }
     if (slab) {
-        if ((rc = join_comm(c))) return rc;  // boundary(t-K) wrote columns the interior reads
-        HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
+        // everything before this cycle, seen from the comm stream: the previous cycle's end on ds
+        // (chained) or the context's stream
+        hipEvent_t before = chained ? c->band_end : c->ev_pre;
         hipStream_t cs = c->comm_stream;
-        if (c->band_x > c->bnd_w) HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_pre, 0));
+        if (c->band_x > c->bnd_w) HIP_TRY(c, hipStreamWaitEvent(cs, before, 0));
         if ((rc = exchange(c, cs, c->band_x))) return rc;
         if (D > 0) HIP_TRY(c, hipEventRecord(c->ev_x, cs));
-        HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_pre, 0));
+        HIP_TRY(c, hipStreamWaitEvent(cs, before, 0));
         Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
         b.vs = c->slab_vs;
         b.variant = c->deep_variant;
@@ -433,35 +472,38 @@ static int band_step(iblb_ctx* c) {
         HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));
     }
-    if (ov) {
-        HIP_TRY(c, hipEventRecord(c->ev_b0, c->stream));
-        HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_b0, 0));
-        HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_b0, 0));
-    }
     if (D > 0) {
         if (slab) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_x, 0));
         else if ((rc = fill_ghosts_periodic(c, c->cur, D, bs))) return rc;
     }
     if ((rc = band_chain<T>(c, K, A, B, S, slab, bs, ds))) return rc;
-    if (ov) {
-        HIP_TRY(c, hipEventRecord(c->ev_b1, ds));
-        HIP_TRY(c, hipEventRecord(c->ev_b2, bs));
-        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b1, 0));
-        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_b2, 0));
-    }
+    // the end of the cycle (ds: deep sweep and last level, after the chain), one marker: the pinned
+    // table slot may be reused once every launch of this cycle has read it, and the next cycle's
+    // chain starts after it (each marker between the last level and the next deep sweep costs ~5 us
+    // of idle queue, profiles/r03ch)
+    c->band_end = c->band_pin_ev[c->band_pin_cur];
+    HIP_TRY(c, hipEventRecord(c->band_end, ds));
+    c->band_run = ov;
     if (slab) {
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->bnd_w = D > 0 ? 0 : K;  // the edge columns of g^{t+K}: the boundary sweeps' unless a trapezoid stored them
         c->deep_chain = false;
     }
-    // the pinned table slot may be reused once every launch of this cycle has read it
-    if (c->band_pin_cur >= 0) HIP_TRY(c, hipEventRecord(c->band_pin_ev[c->band_pin_cur], c->stream));
     c->cur = 1 - c->cur;
     c->t += K;
     c->ghost = 0;
     c->ib_state = IB_PENDING;
     // the force now owed is that of iteration t+K-1's points
     if (c->sch_n > 0) sched_use(c, sched_entry(c, c->t - 1));
+    return IBLB_OK;
+}
+
+// The context's stream after a run of band cycles (before any other step, reader or return).
+int band_join(iblb_ctx* c) {
+    if (!c->band_run) return IBLB_OK;
+    c->band_run = false;
+    // band_end follows the whole cycle: ds waited for the chain (ev_bd) before its last level
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->band_end, 0));
+    if (rccl_multi(c)) HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));  // comm_ready's "last step"
     return IBLB_OK;
 }
 
@@ -474,9 +516,12 @@ int band_release(iblb_ctx* c) {
             (void)hipStreamDestroy(st);
         }
     c->band_st = c->deep_st = nullptr;
-    for (hipEvent_t e : {c->ev_b0, c->ev_b1, c->ev_b2, c->ev_bd})
+    for (hipEvent_t e : {c->ev_b0, c->ev_bd})
         if (e) (void)hipEventDestroy(e);
-    c->ev_b0 = c->ev_b1 = c->ev_b2 = c->ev_bd = nullptr;
+    c->ev_b0 = c->ev_bd = nullptr;
+    c->band_end = nullptr;
+    c->band_run = false;
+    c->band_pin_cur = -1;
     for (int i = 0; i < BAND_PIN_SLOTS; ++i) {
         if (c->band_pin_ev[i]) (void)hipEventDestroy(c->band_pin_ev[i]);
         if (c->band_pin[i]) (void)hipHostFree(c->band_pin[i]);

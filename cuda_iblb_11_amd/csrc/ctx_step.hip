@@ -497,6 +497,7 @@ int iblb_step(iblb_ctx* c, int nsteps) {
             s += K;
             continue;
         }
+        if ((rc = band_join(c))) return rc;
         if (K >= 3 && nsteps - s >= K && sweep_ready(c)) {
             if (single_slab(c)) {
                 if ((rc = is_f64(c) ? sweepk_step<double>(c) : sweepk_step<float>(c))) return rc;
@@ -517,6 +518,7 @@ int iblb_step(iblb_ctx* c, int nsteps) {
         if ((rc = step_one(c))) return rc;
         ++s;
     }
+    if ((rc = band_join(c))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return IBLB_OK;
 }

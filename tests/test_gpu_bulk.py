@@ -95,11 +95,65 @@ def test_m_bulk_perturbed(gpu, oracle, threads):
     assert max(r["rho"], r["ux"], r["uy"]) <= TIGHT, r
 
 
+def _record(name, r):
+    """Achieved f32 parity numbers, kept for DESIGN.md (gpurun_out/parity_f32.json on the GPU box)."""
+    import json
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity_f32.json")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    try:
+        d = json.load(open(path))
+    except Exception:
+        d = {}
+    d[name] = r
+    json.dump(d, open(path, "w"), indent=1)
+
+
 def test_m_bulk_f32(gpu, oracle, threads):
+    """M in f32, 11 iterations (boot + two deep launches); rho - 1 and u each normalised by their
+    own max (f32 stores f - w_i, so rho - 1 is resolved, not rho ~ 1)."""
     lat, sim, tm = bulk_pair(gpu, oracle, 4096, 4096, [11], precision="f32")
     assert tm["sweepk_launches"] == 2, tm
     r = fields(lat, sim)
-    assert max(r["rho"], r["ux"], r["uy"]) <= TOL32, r
+    _record("M_4096_f32_11", r)
+    assert max(r["rho-1"], r["ux"], r["uy"]) <= TOL32, r
+
+
+def test_k1_1000_steps_bulk_f32(gpu, oracle, threads):
+    """f32 over the longest horizon: 128^2, 1000 iterations in one call (199 deep launches).
+    By then rho - 1 has decayed to ~1e-5 while f32 rounding keeps adding ~1e-12 per cell and
+    iteration, so the 1e-4 bound on rho - 1 is below what float32 arithmetic can hold: a plain
+    numpy float32 restatement of the same iteration (tests/f32_model.py) lands at 1.5e-4 on
+    rho - 1 and u_y.  Bound: 1e-4, or twice that f32 floor where the floor itself exceeds it."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from f32_model import F32Channel
+    from cuda_iblb_11_amd import workloads as W
+    lat, sim, tm = bulk_pair(gpu, oracle, 128, 128, [1000], precision="f32")
+    assert tm["sweepk_launches"] >= 190, tm
+    r = fields(lat, sim)
+    rho, u = W.perturbed_state(128, 128, 31)
+    m = F32Channel(128, 128, W.TAU, W.TAU2, rho, u, W.BODY_FORCE)
+    m.step(1000)
+    mr, mu = m.macro()
+    N = 128 * 128
+    floor = {"rho-1": rel(mr - 1, sim.rho - 1), "ux": rel(mu[:N], sim.u[:N]), "uy": rel(mu[N:], sim.u[N:])}
+    _record("K1_128_f32_1000", r)
+    _record("K1_128_f32_1000_numpy_f32_floor", floor)
+    for k, v in floor.items():
+        assert r[k] <= max(TOL32, 2 * v), (k, r, floor)
+    assert abs(lat.flux - sim.flux) <= TOL32 * abs(sim.flux)
+
+
+def test_band_cycle_f32_100_steps(gpu, oracle, threads):
+    """f32 through the IB band cycle over 100 iterations at 2048^2: a 256-point filament whose
+    points move every iteration (it sways across 4 columns), given ahead in chunks of 25."""
+    from cuda_iblb_11_amd import workloads as W
+    pts = lambda it: W.filament(it, n_points=256, x0=1024.3, y0=1.0, dy=1.0, U0=2e-3, period=40, sway=2.0)
+    lat, sim = moving_run(gpu, oracle, 2048, 2048, pts, [25, 25, 25, 25], precision="f32", body_force=W.BODY_FORCE)
+    assert lat.timing()["sweepk_launches"] >= 18
+    r = fields(lat, sim)
+    _record("band_2048_f32_100_moving", r)
+    assert max(r["rho-1"], r["ux"], r["uy"]) <= TOL32, r
 
 
 def _schedule(points, t0, n):
@@ -224,6 +278,7 @@ def test_k5_filament_array_f32(gpu, oracle, threads):
     lat, sim = moving_run(gpu, oracle, 8192, 2048, pts, [11], precision="f32", body_force=W.BODY_FORCE)
     assert lat.timing()["sweepk_launches"] == 2
     r = fields(lat, sim)
+    _record("K5_8192x2048_f32_11_edges", r)
     assert max(r["rho-1"], r["ux"], r["uy"]) <= TOL32, r
 
 
