@@ -73,7 +73,6 @@ struct iblb_ctx {
     int sweep_w = 4, sweep_vs = 2;  // two-iteration sweeps: columns per wave, cells per lane
     int sweep_depth = 5;        // K iterations per deep launch (IBLB_SWEEP_DEPTH; 2 = two-step only)
     int deep_w = 96, deep_vs = 2, deep_variant = 1, deep_balance = 1;  // IBLB_DEEP_W / _VS / _VARIANT / _BALANCE
-    int sweep_map = 2, sweep_alt = 1;  // IBLB_SWEEP_MAP / IBLB_SWEEP_ALT
     int slab_vs = 1;            // cells per lane of a group slab's deep sweeps
     int reserved_cus = 0, ncu = 0;  // CUs kept free of the compute stream (RCCL groups), device CUs
     std::vector<uint32_t> comp_mask;  // the compute stream's CU mask when reserved_cus > 0

@@ -276,13 +276,6 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     c->band_d = bd;
     c->band_x = bx;
     c->band_valid = true;
-    if (env_long("IBLB_DEBUG_PLAN", 0)) {
-        std::fprintf(stderr, "[iblb plan] x_begin %d t %lld: %zu patches", c->x_begin, c->t, b.size());
-        for (auto& p : b) std::fprintf(stderr, " [%d,%d]x[%d,%d]", p[0], p[1], p[2], p[3]);
-        std::fprintf(stderr, " d %d x %d flux %d rows [%d,%d) entries", bd, bx, c->band_flux, c->band_fy0, c->band_fy1);
-        for (int j = 0; j < K; ++j) std::fprintf(stderr, " %d", cnt[j]);
-        std::fprintf(stderr, "\n");
-    }
     return IBLB_OK;
 }
 
@@ -340,7 +333,8 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
 // The band chain as 2K dependent launches on bs: the IB of each level over every point (image)
 // forcing the columns the level computes, then the level's one-step launch over the trapezoid's
 // entries; the deep sweep on ds; the last level after the deep sweep (on ds, right behind it) and,
-// when it stores a slab's edge columns, after the boundary sweeps (ev_bnd).
+// when it stores a slab's edge columns, after the boundary sweeps (ev_bnd).  c->band_end is
+// recorded on ds at the end (by the last level's own completion where it launches).
 template <typename T>
 static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool slab, hipStream_t bs, hipStream_t ds) {
     int rc;
@@ -405,11 +399,12 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
                 ls = ds;
             }
             if (slab && D > 0) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_bnd, 0));
+            if (a.ncols <= 0) HIP_TRY(c, hipEventRecord(c->band_end, ls));
         }
         if (a.ncols <= 0) continue;
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, ls))) return rc;
-        HIP_TRY(c, launch_fused<T>(a, ls));
+        HIP_TRY(c, launch_fused<T>(a, ls, j == K - 1 ? c->band_end : nullptr));
         if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * a.nchl * 64 * c->V, ls))) return rc;
     }
     return IBLB_OK;
@@ -476,13 +471,12 @@ static int band_step(iblb_ctx* c) {
         if (slab) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_x, 0));
         else if ((rc = fill_ghosts_periodic(c, c->cur, D, bs))) return rc;
     }
+    // the end of the cycle (ds: deep sweep and last level, after the chain), recorded by the last
+    // level's completion signal: the pinned table slot may be reused once every launch of this cycle
+    // has read it, and the next cycle's chain starts after it (a marker packet between the last
+    // level and the next deep sweep left ~7 us of idle queue per cycle, profiles/r03ch2)
+    c->band_end = c->band_pin_ev[c->band_pin_cur];  // (the waits above took the previous cycle's)
     if ((rc = band_chain<T>(c, K, A, B, S, slab, bs, ds))) return rc;
-    // the end of the cycle (ds: deep sweep and last level, after the chain), one marker: the pinned
-    // table slot may be reused once every launch of this cycle has read it, and the next cycle's
-    // chain starts after it (each marker between the last level and the next deep sweep costs ~5 us
-    // of idle queue, profiles/r03ch)
-    c->band_end = c->band_pin_ev[c->band_pin_cur];
-    HIP_TRY(c, hipEventRecord(c->band_end, ds));
     c->band_run = ov;
     if (slab) {
         c->bnd_w = D > 0 ? 0 : K;  // the edge columns of g^{t+K}: the boundary sweeps' unless a trapezoid stored them

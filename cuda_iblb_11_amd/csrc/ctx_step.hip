@@ -259,8 +259,6 @@ Sweep2Args<T> sweep_args(iblb_ctx* c, int col_begin, int col_step, int col_end, 
     a.W = W;
     a.vs = c->sweep_vs;
     a.variant = 1;  // nontemporal stores
-    a.map = c->sweep_map ? c->sweep_map : 2;
-    a.alt = c->sweep_alt;
     const int fc = c->cfg.flux_column - c->x_begin;
     a.flux_col = (fc >= 0 && fc < c->ncol) ? fc : -1;
     a.fskip0 = a.fskip1 = 0;

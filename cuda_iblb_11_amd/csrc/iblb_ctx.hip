@@ -241,8 +241,6 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->sweep_on = env_long("IBLB_SWEEP", 1) != 0;
     c->sweep_w = (int)env_long("IBLB_SWEEP_W", f64 ? 4 : 6);
     c->sweep_vs = (int)env_long("IBLB_SWEEP_VS", f64 ? 2 : 4);
-    c->sweep_map = (int)env_long("IBLB_SWEEP_MAP", 2);
-    c->sweep_alt = (int)env_long("IBLB_SWEEP_ALT", 1);
     c->sweep_depth = (int)std::min(6L, std::max(2L, env_long("IBLB_SWEEP_DEPTH", 5)));
     c->deep_w = (int)env_long("IBLB_DEEP_W", f64 ? 96 : 64);
     c->deep_vs = (int)env_long("IBLB_DEEP_VS", 2);

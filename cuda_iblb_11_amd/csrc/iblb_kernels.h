@@ -59,9 +59,6 @@ struct Sweep2Args {
     int vs;              // cells per lane; rows, col and plane multiples of vs
     int nch;             // set by launch_sweep2
     int variant;         // MODE bits (nontemporal loads / stores, no prefetch)
-    int map;             // 1: linear, chunk fastest; 0: 4 sweeps per workgroup, XCD-contiguous;
-                         // 2: linear order in XCD-contiguous ranges (default)
-    int alt;             // odd sweeps walk right to left (neighbours read their shared edges together)
     int cus;             // deep sweeps, balanced widths: CUs the launch's stream may use (0 = all)
     int flux_col;        // local column sampled for Q (every iteration), or -1
     int fskip0, fskip1;  // rows [fskip0, fskip1) of the flux column are not sampled (an IB band
@@ -77,7 +74,7 @@ struct Sweep2Args {
 // columns of the buffer itself (a group slab's boundary sweeps after the halo exchange)
 template <typename T>
 hipError_t launch_sweep2(Sweep2Args<T> a, bool ghost, hipStream_t s);
-// K = depth (3 .. 6) iterations per launch: g^t -> g^{t+K}; map 1 or 2; ghost as above (a
+// K = depth (3 .. 6) iterations per launch: g^t -> g^{t+K}; ghost as above (a
 // boundary sweep of output columns [0, K) reads columns -K .. 2K-1).  col_step 0: balanced widths.
 template <typename T>
 hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool ghost, hipStream_t s);
@@ -89,7 +86,7 @@ int sweepk_geometry(int depth, int vs, int variant, bool ghost, int ny, int* nch
 inline int chunks_per_column(int ny, int V) { return (ny + 64 * V - 1) / (64 * V); }
 
 template <typename T>
-hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s);
+hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s, hipEvent_t stop = nullptr);  // stop: recorded at the end
 
 // Step 0 of a fresh state: collide f^0 with explicit rho^0, u^0, force^0 (no pull).
 template <typename T>

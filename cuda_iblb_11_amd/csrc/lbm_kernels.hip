@@ -6,6 +6,8 @@
 // Reference data flow it replaces: equilibrium -> collision -> streaming -> macro ->
 // spread's u correction (LatticeBoltzmann.cu:30-411, ImmersedBoundary.cu:249-264),
 // ~824 B/LU there.
+#include <hip/hip_ext.h>
+
 #include "lbm_vec.h"
 #include "ib_device.h"
 
@@ -141,29 +143,35 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
 }
 
 template <typename T, int MODE>
-hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t s) {
+hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t s, hipEvent_t stop) {
     constexpr int V = vec_of<T>();
-    if (a.flags)
+    if (stop) {  // the event rides on the kernel's own completion signal: no marker packet after it
+        if (a.flags)
+            hipExtLaunchKernelGGL(fused_kernel<T, V, true, MODE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, a);
+        else
+            hipExtLaunchKernelGGL(fused_kernel<T, V, false, MODE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, a);
+    } else if (a.flags) {
         fused_kernel<T, V, true, MODE><<<blocks, 256, 0, s>>>(a);
-    else
+    } else {
         fused_kernel<T, V, false, MODE><<<blocks, 256, 0, s>>>(a);
+    }
     return hipGetLastError();
 }
 
 template <typename T>
-hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s) {
+hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s, hipEvent_t stop) {
     const long waves = (long)a.ncols * (a.row_tab ? a.nchl : a.nch);
     if (waves <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     switch (a.variant) {
-        case 1: return launch_fused_mode<T, 1>(a, blocks, s);
-        case 2: return launch_fused_mode<T, 2>(a, blocks, s);
-        case 3: return launch_fused_mode<T, 3>(a, blocks, s);
-        case 4: return launch_fused_mode<T, 4>(a, blocks, s);
-        case 5: return launch_fused_mode<T, 5>(a, blocks, s);
-        case 6: return launch_fused_mode<T, 6>(a, blocks, s);
-        case 7: return launch_fused_mode<T, 7>(a, blocks, s);
-        default: return launch_fused_mode<T, 0>(a, blocks, s);
+        case 1: return launch_fused_mode<T, 1>(a, blocks, s, stop);
+        case 2: return launch_fused_mode<T, 2>(a, blocks, s, stop);
+        case 3: return launch_fused_mode<T, 3>(a, blocks, s, stop);
+        case 4: return launch_fused_mode<T, 4>(a, blocks, s, stop);
+        case 5: return launch_fused_mode<T, 5>(a, blocks, s, stop);
+        case 6: return launch_fused_mode<T, 6>(a, blocks, s, stop);
+        case 7: return launch_fused_mode<T, 7>(a, blocks, s, stop);
+        default: return launch_fused_mode<T, 0>(a, blocks, s, stop);
     }
 }
 
@@ -338,7 +346,7 @@ hipError_t launch_field_out(const double* lay, double* ref, Layout L, int ncomp,
 }
 
 #define IBLB_INST(T)                                                                                            \
-    template hipError_t launch_fused<T>(const FusedArgs<T>&, hipStream_t);                                      \
+    template hipError_t launch_fused<T>(const FusedArgs<T>&, hipStream_t, hipEvent_t);                                \
     template hipError_t launch_boot<T>(const T*, T*, Layout, const double*, const double*, const double*, long,  \
                                        Coef, KConst, hipStream_t);                                                  \
     template hipError_t launch_macro_out<T>(const T*, Layout, Halo<T>, const double*, long, double, double,      \

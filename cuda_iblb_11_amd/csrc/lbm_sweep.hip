@@ -46,7 +46,7 @@ hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool slab, hipStream_t s) {
     if (a.nsweep <= 0) return hipSuccess;
     // rows are read from row0 - 1 >= -(K-1) - VS - 1 to the last wave's row0 + 64*VS: inside the
     // 512-element guards of the buffers
-    if (a.W <= 0 || a.L.ncol < 1 || a.vs <= 0 || a.map == 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 ||
+    if (a.W <= 0 || a.L.ncol < 1 || a.vs <= 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 ||
         a.L.col % a.vs != 0)
         return hipErrorInvalidValue;
     return slab ? launch_sweepk_slab<T, true>(a, depth, s) : launch_sweepk_slab<T, false>(a, depth, s);

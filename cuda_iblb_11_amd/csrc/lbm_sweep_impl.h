@@ -276,6 +276,20 @@ __device__ __forceinline__ double sweep_walk(const Sweep2Args<T>& a, int xa, int
     return q;
 }
 
+// wave -> (sweep, chunk), chunk fastest, with that linear order dealt to the eight XCDs in
+// contiguous ranges (blocks b and b+8 share an XCD: the dispatcher deals workgroups round-robin over
+// all eight whatever the stream's CU mask, profiles/r02n_xcc_probe.txt), so the edge columns of
+// neighbouring sweeps are re-read from the L2 that just fetched them.  Odd sweeps walk right to
+// left: neighbours read their shared edge columns at about the same time.
+__device__ __forceinline__ void linear_item(int nch, int wv, int& sw, int& ch) {
+    int b = (int)blockIdx.x;
+    const int q = (int)gridDim.x / 8;
+    if (b < 8 * q) b = (b % 8) * q + b / 8;
+    const int gw = b * 4 + wv;
+    sw = gw / nch;
+    ch = gw - sw * nch;
+}
+
 // One wave = (sweep, chunk).  Lane l holds rows r0 = cs - VS + l*VS .. r0+VS-1: lanes 1..62 own
 // the chunk's 62*VS output rows [cs, cs + 62*VS), lanes 0 and 63 are ghost rows (the g1 values
 // of the rows just outside the chunk that step 2 pulls).  Ghost rows and rows >= ny compute
@@ -287,28 +301,7 @@ __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int sw, ch;
-    if (a.map == 0) {
-        // a workgroup = 4 neighbouring sweeps of one chunk (their shared edge columns are read
-        // once from HBM), workgroups remapped so that each XCD (blocks b = 8*slot + xcd) walks a
-        // contiguous range of (chunk, sweep group): neighbouring groups run on one L2
-        const int nb = (int)gridDim.x, b = (int)blockIdx.x, q = nb / 8;
-        const int work = b < 8 * q ? (b % 8) * q + b / 8 : b;
-        const int ngroups = (a.nsweep + 3) / 4;
-        ch = work / ngroups;
-        sw = (work - ch * ngroups) * 4 + wv;
-    } else {
-        // linear: wave -> (sweep, chunk), chunk fastest.  map 2: the same order dealt to the
-        // XCDs in contiguous ranges (blocks b and b+8 share an XCD), so the edge columns of
-        // neighbouring sweeps are re-read from the L2 that just fetched them
-        int b = (int)blockIdx.x;
-        if (a.map == 2) {
-            const int q = (int)gridDim.x / 8;
-            if (b < 8 * q) b = (b % 8) * q + b / 8;
-        }
-        const int gw = b * 4 + wv;
-        sw = gw / a.nch;
-        ch = gw - sw * a.nch;
-    }
+    linear_item(a.nch, wv, sw, ch);
     if (sw >= a.nsweep || ch >= a.nch) return;
     const int xa = a.col_begin + sw * a.col_step;
     const int xb = min(xa + a.W, a.col_end);
@@ -320,7 +313,7 @@ __global__ __launch_bounds__(256) void sweep2_kernel(Sweep2Args<T> a) {
     const bool owner = lane >= 1 && lane <= 62 && r0 < a.L.ny;
     const bool bot = r0 == 0;
     const bool top = et >= 0 && et < VS;
-    const double q = (a.alt && (sw & 1))
+    const double q = (sw & 1)
                          ? sweep_walk<T, VS, MODE, SLAB, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
                          : sweep_walk<T, VS, MODE, SLAB, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top);
     if (a.flux_col >= xa && a.flux_col < xb) {
@@ -351,8 +344,7 @@ hipError_t launch_sweep2(Sweep2Args<T> a, bool slab, hipStream_t s) {
     if (a.W <= 0 || a.L.ncol < 2 || a.vs <= 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 || a.L.col % a.vs != 0)
         return hipErrorInvalidValue;
     a.nch = (a.L.ny + 62 * a.vs - 1) / (62 * a.vs);
-    const unsigned blocks = a.map == 0 ? (unsigned)(((a.nsweep + 3) / 4) * (long)a.nch)
-                                       : (unsigned)(((long)a.nsweep * a.nch + 3) / 4);
+    const unsigned blocks = (unsigned)(((long)a.nsweep * a.nch + 3) / 4);
     constexpr int V = vec_of<T>();
     if (a.vs == V) return launch_sweep_vs<T, V>(a, slab, blocks, s);
     if (a.vs == V / 2) return launch_sweep_vs<T, V / 2>(a, slab, blocks, s);
@@ -639,20 +631,6 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
     return q;
 }
 
-// wave -> (sweep, chunk) of the linear order, optionally (map 2) dealt to the eight XCDs in
-// contiguous ranges (the dispatcher deals workgroups round-robin over all eight whatever the
-// stream's CU mask, profiles/r02n_xcc_probe.txt)
-__device__ __forceinline__ void linear_item(int map, int nch, int wv, int& sw, int& ch) {
-    int b = (int)blockIdx.x;
-    if (map == 2) {
-        const int q = (int)gridDim.x / 8;
-        if (b < 8 * q) b = (b % 8) * q + b / 8;
-    }
-    const int gw = b * 4 + wv;
-    sw = gw / nch;
-    ch = gw - sw * nch;
-}
-
 template <int K, int VS>
 constexpr int ghost_lanes() { return (K - 1 + VS - 1) / VS; }
 
@@ -664,7 +642,7 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int sw, ch;
-    linear_item(a.map, a.nch, wv, sw, ch);
+    linear_item(a.nch, wv, sw, ch);
     if (sw >= a.nsweep || ch >= a.nch) return;
     int xa, xb;
     if (a.col_step > 0) {
@@ -685,7 +663,7 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
     const bool top = et >= 0 && et < VS;
     // wave-uniform: does the wave hold a wall row (y = 0 or Y-1, ghost lanes included)?
     const bool walls = row0 <= 0 || row0 + 64 * VS >= a.L.ny;
-    const bool rev = a.alt && (sw & 1);
+    const bool rev = sw & 1;
     const double q =
         walls ? (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
                      : sweepk_walk<T, VS, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top))

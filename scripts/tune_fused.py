@@ -52,7 +52,7 @@ def main():
             sets.append((grp, e))
     names = sorted({k for _, e in sets for k in e} | {"IBLB_FUSED_VARIANT", "IBLB_PLANE_PAD", "IBLB_BUF_GAP",
                                                      "IBLB_SWEEP", "IBLB_SWEEP_W", "IBLB_SWEEP_VS", "IBLB_SWEEP_VARIANT",
-                                                     "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT", "IBLB_SWEEP_DEPTH",
+                                                     "IBLB_SWEEP_DEPTH",
                                                      "IBLB_DEEP_W", "IBLB_DEEP_VS", "IBLB_DEEP_VARIANT", "IBLB_DEEP_BALANCE"})
     ctxs = []
     for key, e in sets:

@@ -491,14 +491,11 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
         monkeypatch.setenv("IBLB_SWEEP", "1")
         monkeypatch.setenv("IBLB_SWEEP_DEPTH", str(depth))
         for vs in vss:
-            for w, var, mp, alt, bal in [(4, 1, 2, 1, 0), (1, 0, 1, 0, 0), (3, 1, 2, 0, 1), (32, 1, 1, 1, 0),
-                                         (7, 0, 2, 1, 1), (48, 1, 2, 1, 1)]:
+            for w, var, bal in [(4, 1, 0), (1, 0, 0), (3, 1, 1), (32, 1, 0), (7, 0, 1), (48, 1, 1)]:
                 monkeypatch.setenv("IBLB_DEEP_VS", str(vs))
                 monkeypatch.setenv("IBLB_DEEP_W", str(w))
                 monkeypatch.setenv("IBLB_DEEP_VARIANT", str(var))
                 monkeypatch.setenv("IBLB_DEEP_BALANCE", str(bal))
-                monkeypatch.setenv("IBLB_SWEEP_MAP", str(mp))
-                monkeypatch.setenv("IBLB_SWEEP_ALT", str(alt))
                 lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 3e-7))
                 lat.set_state(rho, u)
                 lat.set_profiling(True)
@@ -506,12 +503,11 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
                 tm = lat.timing()
                 assert tm["sweepk_launches"] == 10 and tm["sweep_launches"] == 1 and tm["sweepk_depth"] == depth, tm
                 f = lat.populations()
-                assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, mp, alt, bal,
+                assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, bal,
                                                   float(np.max(np.abs(f - f_ref))))
                 assert abs(lat.flux - q_ref) <= 1e-12 * abs(q_ref), (lat.flux, q_ref)
                 lat.close()
-    for name in ("IBLB_SWEEP_DEPTH", "IBLB_DEEP_VS", "IBLB_DEEP_W", "IBLB_DEEP_VARIANT", "IBLB_DEEP_BALANCE",
-                 "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT"):
+    for name in ("IBLB_SWEEP_DEPTH", "IBLB_DEEP_VS", "IBLB_DEEP_W", "IBLB_DEEP_VARIANT", "IBLB_DEEP_BALANCE"):
         monkeypatch.delenv(name)
 
 
@@ -519,7 +515,7 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
 def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch):
     """The two-iteration sweep kernel (g1 kept in registers, ghost lanes for the chunk edges,
     periodic columns) equals pairs of one-step launches bit for bit, for every cells-per-lane
-    width, sweep length, wave mapping and walking direction, on shapes with ragged chunks (ny not a multiple of
+    width and sweep length (odd sweeps walk right to left), on shapes with ragged chunks (ny not a multiple of
     62*VS), fewer columns than one sweep, one-row-above-a-chunk tops and several chunks; odd step
     counts end with a one-step launch.  Flux: same terms, other summation order."""
     from cuda_iblb_11_amd import workloads as W
@@ -535,14 +531,11 @@ def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch)
         ref.close()
         monkeypatch.setenv("IBLB_SWEEP", "1")
         for vs in vss:
-            for w, mp, alt in [(1, 1, 0), (3, 1, 1), (32, 1, 0), (8, 2, 0), (3, 2, 1), (5, 1, 0), (1, 2, 1),
-                               (7, 1, 0), (32, 2, 1), (4, 2, 0), (4, 2, 1), (6, 1, 1)]:
+            for w in [1, 3, 32, 8, 5, 7, 4, 6]:
                 if True:
                     var = 1
                     monkeypatch.setenv("IBLB_SWEEP_VS", str(vs))
                     monkeypatch.setenv("IBLB_SWEEP_W", str(w))
-                    monkeypatch.setenv("IBLB_SWEEP_MAP", str(mp))
-                    monkeypatch.setenv("IBLB_SWEEP_ALT", str(alt))
                     lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 3e-7))
                     lat.set_state(rho, u)
                     lat.set_profiling(True)
@@ -550,10 +543,10 @@ def test_sweep_two_iterations_bit_identical(gpu, oracle, precision, monkeypatch)
                     tm = lat.timing()
                     assert tm["sweep_launches"] == 15 and tm["fused_launches"] == 1, tm
                     f = lat.populations()
-                    assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, mp, alt, float(np.max(np.abs(f - f_ref))))
+                    assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, float(np.max(np.abs(f - f_ref))))
                     assert abs(lat.flux - q_ref) <= 1e-12 * abs(q_ref), (lat.flux, q_ref)
                     lat.close()
-    for name in ("IBLB_SWEEP_VS", "IBLB_SWEEP_W", "IBLB_SWEEP_MAP", "IBLB_SWEEP_ALT", "IBLB_SWEEP_DEPTH"):
+    for name in ("IBLB_SWEEP_VS", "IBLB_SWEEP_W", "IBLB_SWEEP_DEPTH"):
         monkeypatch.delenv(name)
     # (run_pair steps one iteration per call: one-step launches vs the oracle; the sweeps against
     # the oracle in bulk: tests/test_gpu_bulk.py)
