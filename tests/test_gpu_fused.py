@@ -607,6 +607,23 @@ def test_ib_band_cycle_matches_oracle(gpu, oracle, precision, monkeypatch):
     assert abs(lat.flux - sim.flux) <= (1e-9 if precision == "f64" else 1e-4) * max(abs(sim.flux), 1e-30)
 
 
+@pytest.mark.parametrize("band_cus", ["0", "8", "-2"])
+def test_ib_band_stream_arrangements(gpu, oracle, band_cus, monkeypatch):
+    """The band cycle's stream arrangements (IBLB_BAND_CUS): the chain and the deep sweep in sequence
+    on one stream (0), on two CU-masked streams (8 CUs for the chain), on two unmasked streams with
+    the chain's at the highest priority (-2, the default of lone slabs with long deep sweeps).
+    Consecutive cycles stay on the band streams (joined when the run of cycles ends); chunked calls
+    with one-step remainders between the runs of cycles exercise the joins."""
+    monkeypatch.setenv("IBLB_BAND_CUS", band_cus)
+    nx, ny = 256, 160
+    a, b = _line(64.37, 60), _line(171.6, 48, y0=20.0)
+    pts = tuple(np.concatenate([p, q]) for p, q in zip(a, b))
+    lat, sim = _static_run(gpu, oracle, nx, ny, 38, pts, chunks=(1, 10, 12, 15), monkeypatch=monkeypatch)
+    assert lat.timing()["sweepk_launches"] >= 6
+    check_fields(lat, sim, 1e-10)
+    assert abs(lat.flux - sim.flux) <= 1e-9 * max(abs(sim.flux), 1e-30)
+
+
 @pytest.mark.parametrize("x0", [246.2, 243.8, 200.0])
 def test_ib_band_flux_column(gpu, oracle, x0, monkeypatch):
     """Flux column XDIM-5 = 251 inside a band's output (x0 = 246), inside its trapezoid ghost
