@@ -112,6 +112,7 @@ struct iblb_ctx {
     long long sch_t0 = 0;
     std::vector<float> sch_x;       // [sch_n][ns][2]: (x, y) of every entry (band plans)
     std::vector<float> sch_x_prev;  // the points before the schedule (their force may be owed)
+    bool cil_sched = false;         // the schedule is the cilia kinematics run ahead (cilia_schedule)
     // dense IB force [2][(ncol + 2 gc) * rows] and a flag per (column, row chunk); fdense and
     // flags point at column 0
     double* fd_alloc = nullptr;
@@ -134,6 +135,7 @@ struct iblb_ctx {
     long long band_deep_lu = 0, band_lu = 0;       // cells of the deep sweep / of all trapezoid levels
     int band_flux = -1, band_fy0 = 0, band_fy1 = 0;  // flux column in a patch output, the patch's rows
     bool band_run = false;       // the last step was a band cycle on band_st / deep_st (not joined)
+    long long band_retry_t = 0;  // a declined schedule plan: next attempt at this iteration
     hipEvent_t band_end = nullptr; // recorded on the deep stream at the end of the last band cycle
     char* s_alloc = nullptr;     // two scratch population buffers of the trapezoid (layout of g)
     void* sbuf[2] = {nullptr, nullptr};
@@ -299,6 +301,10 @@ int band_step_any(iblb_ctx* c);
 int plan_bands(iblb_ctx* c, const std::vector<float>& xy);
 int plan_cycle(iblb_ctx* c);
 int band_join(iblb_ctx* c);     // the context's stream after a run of band cycles
+int retire_points(iblb_ctx* c);  // owed force evaluated; an active schedule entry becomes the static points
+int cilia_schedule(iblb_ctx* c, int n);  // cilia kinematics of the next n iterations as a schedule
+int cilia_schedule_end(iblb_ctx* c);
+bool band_possible(const iblb_ctx* c);  // the band cycle may run on this context (points aside)
 int band_release(iblb_ctx* c);  // streams, events, pinned tables, scratch buffers
 
 }  // namespace iblbh

@@ -45,7 +45,12 @@ static bool band_slab_ok(const iblb_ctx* c) {
 
 bool band_ready(const iblb_ctx* c) {
     return c->band_on && c->band_valid && (single_slab(c) || band_slab_ok(c)) && c->phase == PH_RUN &&
-           !c->cilia_on && ib_active(c) && c->sweep_on && c->sweep_depth >= 3;
+           (!c->cilia_on || c->cil_sched) && ib_active(c) && c->sweep_on && c->sweep_depth >= 3;
+}
+
+bool band_possible(const iblb_ctx* c) {
+    return c->band_on && c->sweep_on && c->sweep_depth >= 3 && c->phase != PH_EMPTY &&
+           (single_slab(c) || band_slab_ok(c));
 }
 
 // Streams of the overlapped band cycle: the band chain on band_st restricted to `band_reserve` CUs
@@ -281,7 +286,7 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
 
 int plan_bands(iblb_ctx* c, const std::vector<float>& xy) {
     c->band_dirty = false;
-    if (!c->band_on || xy.empty() || c->sweep_depth < 3 || !c->sweep_on || c->cilia_on ||
+    if (!c->band_on || xy.empty() || c->sweep_depth < 3 || !c->sweep_on || (c->cilia_on && !c->cil_sched) ||
         !(single_slab(c) || band_slab_ok(c))) {
         c->band_valid = false;
         return IBLB_OK;

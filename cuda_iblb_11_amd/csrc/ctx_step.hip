@@ -432,7 +432,7 @@ int run_cilia(iblb_ctx* c) {
 static int step_one(iblb_ctx* c) {
     int rc = join_comm(c);
     if (rc) return rc;
-    if (c->cilia_on) {
+    if (c->cilia_on && !c->cil_sched) {
         if (c->phase == PH_RUN && ((rc = ensure_halo(c)) || (rc = ensure_force(c)))) return rc;
         if ((rc = run_cilia(c))) return rc;
     } else if (c->phase == PH_RUN && rccl_multi(c) && c->overlap && c->ib_state == IB_PENDING && c->ghost < 3 &&
@@ -477,17 +477,20 @@ using namespace iblbh;
 
 extern "C" {
 
-int iblb_step(iblb_ctx* c, int nsteps) {
-    if (!c || nsteps < 0) return IBLB_ERR_ARG;
-    if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: use iblb_group_step");
-    int rc = check_ready(c);
-    if (rc) return rc;
-    HIP_TRY(c, hipSetDevice(c->device));
+// nsteps iterations by the fastest applicable schedule per iteration (band cycles, deep sweeps,
+// two-iteration sweeps, one-step iterations); the band streams may still run at the end
+static int step_range(iblb_ctx* c, int nsteps) {
+    int rc = IBLB_OK;
     const int K = c->sweep_depth;
     for (int s = 0; s < nsteps;) {
-        if (nsteps - s >= K && c->phase == PH_RUN && !c->cilia_on && K >= 3) {
-            if (c->sch_n > 0) rc = plan_cycle(c);
-            else if (c->band_dirty) rc = plan_bands(c, c->pts_host);
+        if (nsteps - s >= K && c->phase == PH_RUN && (!c->cilia_on || c->cil_sched) && K >= 3) {
+            // a schedule's cycle whose plan was declined (trapezoids over half the lattice) is
+            // planned again K iterations later, not at every one-step iteration in between
+            if (c->sch_n > 0 && c->t >= c->band_retry_t) {
+                if (!(rc = plan_cycle(c)) && !c->band_valid) c->band_retry_t = c->t + K;
+            } else if (c->band_dirty) {
+                rc = plan_bands(c, c->pts_host);
+            }
             if (rc) return rc;
         }
         if (nsteps - s >= K && band_ready(c)) {
@@ -515,6 +518,29 @@ int iblb_step(iblb_ctx* c, int nsteps) {
         }
         if ((rc = step_one(c))) return rc;
         ++s;
+    }
+    return IBLB_OK;
+}
+
+int iblb_step(iblb_ctx* c, int nsteps) {
+    if (!c || nsteps < 0) return IBLB_ERR_ARG;
+    if (c->transport == TR_LOCAL) return fail(c, IBLB_ERR_STATE, "local group: use iblb_group_step");
+    int rc = check_ready(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const int K = c->sweep_depth;
+    // on-device cilia: the kinematics of up to CILIA_AHEAD iterations run ahead as a schedule, so
+    // that the band cycle applies (cilia_schedule); otherwise one kinematics launch per iteration
+    constexpr int CILIA_AHEAD = 500;
+    for (int done = 0; done < nsteps;) {
+        int seg = nsteps - done;
+        if (c->cilia_on && seg >= K && band_possible(c)) {
+            seg = std::min(seg, CILIA_AHEAD);
+            if ((rc = cilia_schedule(c, seg)) || (rc = step_range(c, seg)) || (rc = cilia_schedule_end(c))) return rc;
+        } else if ((rc = step_range(c, seg))) {
+            return rc;
+        }
+        done += seg;
     }
     if ((rc = band_join(c))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));

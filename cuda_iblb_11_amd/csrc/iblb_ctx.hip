@@ -126,7 +126,7 @@ static std::vector<float> host_points(const float* s, size_t ns) { return std::v
 // an RCCL group), after the comm stream's work of the last step (a one-step IB on the
 // comm stream may still read the schedule arrays, and an RCCL exchange there must precede this
 // one); afterwards the arrays may be rewritten on the context's stream.
-static int retire_points(iblb_ctx* c) {
+int retire_points(iblb_ctx* c) {
     int rc = join_comm(c);
     if (rc) return rc;
     if (c->ib_state == IB_PENDING) {
@@ -146,6 +146,74 @@ static int retire_points(iblb_ctx* c) {
     c->sch_n = 0;
     c->sch_cur = -1;
     return IBLB_OK;
+}
+
+// device arrays of a schedule of n entries of the context's max_points
+static int sched_reserve(iblb_ctx* c, size_t n, int ns) {
+    if (n <= c->sch_cap && ns == c->ns) return IBLB_OK;
+    for (void* p : {(void*)c->d_sch_s, (void*)c->d_sch_us, (void*)c->d_sch_eps})
+        if (p) (void)hipFree(p);
+    c->d_sch_s = c->d_sch_us = nullptr;
+    c->d_sch_eps = nullptr;
+    c->sch_cap = 0;
+    const size_t cap = n * c->max_points;
+    HIP_TRY(c, hipMalloc(&c->d_sch_s, 2 * cap * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&c->d_sch_us, 2 * cap * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&c->d_sch_eps, cap * sizeof(int)));
+    c->sch_cap = n;
+    return IBLB_OK;
+}
+
+// The reference's cilia kinematics (main.cu:822-841) of iterations t .. t+n-1 run ahead on the
+// device into a schedule (the kinematics depend on `it` and on their own previous positions only,
+// not on the fluid), so that iblb_step can take the IB band cycle with on-device cilia: one
+// device-to-host copy of the n entries' positions for the cycles' band plans instead of the
+// schedule upload of iblb_set_lagrangian_steps.  The schedule is retired (its last entry becomes
+// the current points) when the n iterations are done (cilia_schedule_end).
+int cilia_schedule(iblb_ctx* c, int n) {
+    int rc = retire_points(c);  // the force owed to the current points first
+    if (rc) return rc;
+    const iblb_cilia& k = c->cilia;
+    const int ns = CILIA_POINTS * k.c_num;
+    c->sch_x_prev.clear();
+    if (c->ns > 0 && c->ib_state == IB_READY) {  // a force from the current points is owed to iteration t
+        c->sch_x_prev.resize(2 * (size_t)c->ns);
+        HIP_TRY(c, hipMemcpyAsync(c->sch_x_prev.data(), c->d_s, 2 * (size_t)c->ns * sizeof(float), hipMemcpyDeviceToHost,
+                                  c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if ((rc = sched_reserve(c, (size_t)n, ns))) return rc;
+    const size_t per = (size_t)ns;  // entries packed at the points' count (sched_ptr)
+    for (int i = 0; i < n; ++i) {
+        const int it = (int)(c->t + i);
+        HIP_TRY(c, launch_define_filament(k.T, it, k.c_space, k.p_step, (double)k.c_num, c->cil_samples, c->cil_lasts,
+                                          c->cil_bpoints, c->stream));
+        HIP_TRY(c, launch_boundary_check(k.c_space, k.c_num, c->nx, it, c->cil_bpoints, c->d_sch_s + 2 * per * i,
+                                         c->d_sch_us + 2 * per * i, c->d_sch_eps + per * i, c->stream));
+    }
+    // the entries' (x, y) for the band plans
+    c->sch_x.resize(2 * per * (size_t)n);
+    HIP_TRY(c, hipMemcpyAsync(c->sch_x.data(), c->d_sch_s, c->sch_x.size() * sizeof(float), hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->ns = ns;
+    c->sch_t0 = c->t;
+    c->sch_n = n;
+    c->sch_cur = -1;  // d_s holds the points before the schedule
+    c->cil_sched = true;
+    c->band_sticky = true;
+    c->band_valid = false;
+    c->band_retry_t = 0;
+    c->band_dirty = false;
+    return IBLB_OK;
+}
+
+int cilia_schedule_end(iblb_ctx* c) {
+    if (!c->cil_sched) return IBLB_OK;
+    c->cil_sched = false;
+    int rc = band_join(c);
+    if (rc) return rc;
+    return retire_points(c);  // the last entry becomes the current points (d_s, for readers and the next call)
 }
 
 static int check_slab_points(iblb_ctx* c, size_t np, const float* s) {
@@ -445,18 +513,7 @@ int iblb_set_lagrangian_steps(iblb_ctx* c, int nsteps, int ns, const float* s, c
     if (c->ns > 0 && c->ib_state == IB_READY) c->sch_x_prev = c->pts_host;
     if (ns > 0) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        if ((size_t)nsteps > c->sch_cap || ns != c->ns) {
-            for (void* p : {(void*)c->d_sch_s, (void*)c->d_sch_us, (void*)c->d_sch_eps})
-                if (p) (void)hipFree(p);
-            c->d_sch_s = c->d_sch_us = nullptr;
-            c->d_sch_eps = nullptr;
-            c->sch_cap = 0;
-            const size_t cap = (size_t)nsteps * c->max_points;
-            HIP_TRY(c, hipMalloc(&c->d_sch_s, 2 * cap * sizeof(float)));
-            HIP_TRY(c, hipMalloc(&c->d_sch_us, 2 * cap * sizeof(float)));
-            HIP_TRY(c, hipMalloc(&c->d_sch_eps, cap * sizeof(int)));
-            c->sch_cap = (size_t)nsteps;
-        }
+        if ((rc = sched_reserve(c, (size_t)nsteps, ns))) return rc;
         HIP_TRY(c, hipMemcpyAsync(c->d_sch_s, s, 2 * np * sizeof(float), hipMemcpyHostToDevice, c->stream));
         HIP_TRY(c, hipMemcpyAsync(c->d_sch_us, u_s, 2 * np * sizeof(float), hipMemcpyHostToDevice, c->stream));
         if (epsilon) {
@@ -474,6 +531,7 @@ int iblb_set_lagrangian_steps(iblb_ctx* c, int nsteps, int ns, const float* s, c
     c->sch_cur = -1;  // d_s holds the points before the schedule (retire_points)
     c->band_sticky = true;
     c->band_valid = false;  // planned per cycle (plan_cycle)
+    c->band_retry_t = 0;
     c->band_dirty = false;
     return IBLB_OK;
 }
@@ -871,6 +929,7 @@ int iblb_load_checkpoint(iblb_ctx* c, const char* path) {
     c->sch_cur = -1;
     c->band_sticky = false;
     c->band_valid = false;
+    c->band_retry_t = 0;
     c->pts_host.clear();
     if (ns > 0 && !c->cilia_on) {  // host copy for the band plan of the restored points
         c->pts_host.resize(2 * ns);

@@ -335,6 +335,44 @@ def test_reference_cilia_scenario(gpu, oracle, precision):
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_cilia_band_cycle(gpu, oracle, precision, monkeypatch):
+    """On-device cilia through the IB band cycle (round 3): iblb_step runs the kinematics of the
+    call's iterations ahead as a schedule and then K iterations per cycle.  8 cilia 128 apart on
+    1024 x 192, 23 iterations in chunks (1, 20, 2): boot, four band cycles, one-step remainders with
+    the kinematics launched per iteration again; against the oracle fed by the restated kinematics
+    and against the one-step path (IBLB_IB_BAND=0)."""
+    from cuda_iblb_11_amd import workloads as W
+    c_num, c_space, T = 8, 128.0, 100000
+    nx, ny, steps = int(c_num * c_space), 192, 23
+    p_step = T // c_num
+    sim = oracle.Simulation(nx, ny, W.TAU, W.TAU2)
+    cil = oracle.Cilia(c_num, c_space, T, p_step, nx)
+    for it in range(steps):
+        sim.set_lagrangian(*cil.points(it))
+        sim.step(1)
+    out = {}
+    for band in ("1", "0"):
+        monkeypatch.setenv("IBLB_IB_BAND", band)
+        lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, max_points=96 * c_num)
+        lat.set_state()
+        lat.set_cilia(c_num, c_space, T, p_step)
+        lat.set_profiling(True)
+        for n in (1, 20, 2):
+            lat.step(n)
+        s_g, us_g, eps_g = lat.lagrangian()
+        assert np.array_equal(s_g, cil.s) and np.array_equal(us_g, cil.u_s) and np.array_equal(eps_g, cil.epsilon)
+        rho, u = lat.macro()
+        r = fields_rel(rho, u, sim.rho, sim.u, lat.N)
+        assert max(r["rho"], r["ux"], r["uy"]) <= (1e-9 if precision == "f64" else TOL32), (band, r)
+        assert abs(lat.flux - sim.flux) <= (1e-9 if precision == "f64" else 1e-3) * abs(sim.flux)
+        out[band] = (rho, u, lat.timing()["sweepk_launches"])
+        lat.close()
+    assert out["1"][2] >= 4 and out["0"][2] == 0, (out["1"][2], out["0"][2])
+    if precision == "f64":
+        assert rel(out["1"][0], out["0"][0]) <= 1e-13 and rel(out["1"][1], out["0"][1]) <= 1e-11
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("ib", ["none", "cilia"])
 def test_checkpoint_restart(gpu, tmp_path, precision, ib):
     """iblb_save_checkpoint / iblb_load_checkpoint: a fresh context restored mid-run and stepped
