@@ -481,7 +481,7 @@ __device__ __forceinline__ void load_raw_periodic(const Sweep2Args<T>& a, int x,
 template <typename T, int VS, int DX>
 __device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (&B)[9][VS], const T (&C)[9][VS],
                                                   const Sweep2Args<T>& a, int lane, int r0, int et, bool walls,
-                                                  bool flux, bool owner, double& q, T (&out)[9][VS]) {
+                                                  bool flux, int fown, double& q, T (&out)[9][VS]) {
     typedef typename Calc<T>::R R;
     constexpr bool DEV = Store<T>::dev;
     const T(*pk[9])[VS];
@@ -497,7 +497,7 @@ __device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (
         const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
         if (flux) {  // wave-uniform branch; the lane condition as a select (no exec-mask branch)
             const double t = (double)ux / a.flux_norm;
-            q += (owner && flux_row(a, r0 + e)) ? t : 0.;
+            q += ((fown >> e) & 1) ? t : 0.;
         }
 #pragma unroll
         for (int k = 0; k < 9; ++k) out[k][e] = (T)f[k];
@@ -507,7 +507,7 @@ __device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (
 // level 1 of one column from its loaded g^t rows
 template <typename T, int VS>
 __device__ __forceinline__ void level_from_raw(const Raw<T, VS>& cur, const Sweep2Args<T>& a, int lane, int r0, int et,
-                                               bool walls, bool flux, bool owner, double& q, T (&out)[9][VS]) {
+                                               bool walls, bool flux, int fown, double& q, T (&out)[9][VS]) {
     typedef typename Calc<T>::R R;
     constexpr bool DEV = Store<T>::dev;
     const T(*pk[9])[VS];
@@ -526,7 +526,7 @@ __device__ __forceinline__ void level_from_raw(const Raw<T, VS>& cur, const Swee
         const R ux = relax_cell<R, DEV>(f, kbase<R>(a.k), kbody<R>(a.k));
         if (flux) {  // wave-uniform branch; the lane condition as a select (no exec-mask branch)
             const double t = (double)ux / a.flux_norm;
-            q += (owner && flux_row(a, r0 + e)) ? t : 0.;
+            q += ((fown >> e) & 1) ? t : 0.;
         }
 #pragma unroll
         for (int k = 0; k < 9; ++k) out[k][e] = (T)f[k];
@@ -554,12 +554,12 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
                                             unsigned off, int lane, int r0, int et, bool owner, bool bot, bool top,
                                             bool walls, T (&WA)[K - 1][9][VS], T (&WB)[K - 1][9][VS],
                                             Raw<T, VS>& cur, double& q, const BufOfs& bo,
-                                            __amdgpu_buffer_rsrc_t (&rc)[3], bool fin, int fi) {
+                                            __amdgpu_buffer_rsrc_t (&rc)[3], bool fin, int fi, int fown) {
     constexpr int DX = REV ? -1 : 1;
     const int x = x0 + i * DX;
     T N[9][VS];
     // fin: the flux column is one of the sweep's outputs; level l reaches it at step fi + l - 1
-    level_from_raw<T, VS>(cur, a, lane, r0, et, walls, fin && i == fi, owner, q, N);
+    level_from_raw<T, VS>(cur, a, lane, r0, et, walls, fin && i == fi, fown, q, N);
     if (i + 1 < nl1) {
         // the resources of the next column triple: one new column
         if (DX > 0) {
@@ -579,7 +579,7 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
         const bool flux = fin && i == fi + l - 1;
         T out[9][VS];
         const bool made = i >= 2 * (l - 1);
-        if (made) level_from_window<T, VS, DX>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, owner, q, out);
+        if (made) level_from_window<T, VS, DX>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, fown, q, out);
         // level K's columns of the made steps are exactly the sweep's outputs [xa, xb)
         if (made && l == K && owner) {
             const __amdgpu_buffer_rsrc_t rd = col_rsrc<T>(a.dst + (long)c * a.L.col);
@@ -623,11 +623,17 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
     load_raw_periodic<T, VS, MODE, SLAB, K>(a, x0, row0, off, bot, top, cur, bo, rc);
     const bool fin = a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb;
     const int fi = REV ? xb + K - 2 - a.flux_col : a.flux_col - xa + K - 1;  // step of level 1 at the flux column
+    // bit e: row r0 + e is owned and its flux sampled; one VGPR computed once (testing the IB
+    // band's skipped flux rows inside the walk's flux branch changed the compiled loop: +2 % per
+    // launch, profiles/r03ab)
+    int fown = 0;
+#pragma unroll
+    for (int e = 0; e < VS; ++e) fown |= (owner && flux_row(a, r0 + e)) ? 1 << e : 0;
     // (a main loop without the per-level `made` checks, after 2(K-1) window-filling iterations,
     // lets the compiler hoist the collide constants into registers: VGPR spills, 512 VGPRs)
     for (int i = 0; i < nl1; ++i)
         sweepk_iter<T, VS, MODE, K, SLAB, REV>(a, i, nl1, x0, xa, xb, row0, off, lane, r0, et, owner, bot, top, walls, WA,
-                                               WB, cur, q, bo, rc, fin, fi);
+                                               WB, cur, q, bo, rc, fin, fi, fown);
     return q;
 }
 
