@@ -75,6 +75,7 @@ struct iblb_ctx {
     int deep_w = 96, deep_vs = 2, deep_variant = 1, deep_balance = 1;  // IBLB_DEEP_W / _VS / _VARIANT / _BALANCE
     int slab_vs = 1;            // cells per lane of a group slab's deep sweeps
     int reserved_cus = 0, ncu = 0;  // CUs kept free of the compute stream (RCCL groups), device CUs
+    int spare_slots = 0;            // without reserved CUs: wave slots the interior sweeps leave free
     std::vector<uint32_t> comp_mask;  // the compute stream's CU mask when reserved_cus > 0
     hipStream_t stream = nullptr;
     iblb::Coef coef{};
@@ -166,6 +167,7 @@ struct iblb_ctx {
     hipStream_t rccl_last = nullptr;    // the stream of the last RCCL call (ops stay in issue order)
     hipEvent_t ev_bnd = nullptr;  // comm-stream work of the last step done
     hipEvent_t ev_int = nullptr;  // compute-stream work of the last step done
+    hipEvent_t ev_int2 = nullptr; // spare: a deep slab cycle's interior signals it on completion
     hipEvent_t ev_pre = nullptr;  // compute-stream work before this step
     hipEvent_t ev_x = nullptr;    // the band cycle's halo exchange done
     hipEvent_t ev_rccl = nullptr; // orders RCCL calls across streams

@@ -350,13 +350,14 @@ static int sweepk_step(iblb_ctx* c) {
 // K = sweep_depth iterations per cycle on a slab of an RCCL group (ncol >= 2K): K ghost columns
 // exchanged and the boundary sweeps (output columns [0, K) and [ncol-K, ncol), which read columns
 // -K .. 2K-1 and ncol-2K .. ncol+K-1) on the comm stream beside the interior sweep [K, ncol-K):
-//   compute: (join_comm: boundary(t-K)) -> [ev_int] -> interior(t) -> ev_int
-//   comm:    exchange(t) -> wait ev_int (interior(t-K), which read the columns boundary(t)
-//            overwrites) -> boundary(t) -> ev_bnd
+//   compute: (join_comm: boundary(t-K)) -> interior(t) -> ev_int
+//   comm:    exchange(t) -> wait interior(t-K) (it read the columns boundary(t) overwrites) ->
+//            boundary(t) -> ev_bnd
 // The host submits the interior first: the launch the cycle time depends on leaves the host before
-// the RCCL group and the boundary launch.  Cycles back to back: the previous cycle recorded ev_int
-// right after interior(t-K), so the compute stream carries one wait and one record per cycle (each
-// cross-queue packet idles the compute queue for microseconds, profiles/r02q_*).
+// the RCCL group and the boundary launch.  The interior and boundary launches signal ev_int / ev_bnd
+// with their own completion signals (no marker packets: each cross-queue packet idles a queue for
+// microseconds, profiles/r02q_*); the interior's event alternates between ev_int and ev_int2, so
+// the comm stream's waits still name interior(t-K) while interior(t) is in flight.
 // (IBLB_OVERLAP=0: exchange, boundary and interior in sequence on the compute stream.)
 template <typename T>
 static int deep_slab_step(iblb_ctx* c) {
@@ -367,39 +368,45 @@ static int deep_slab_step(iblb_ctx* c) {
     if (rc) return rc;
     hipStream_t bs = ov ? c->comm_stream : c->stream;
     const int ni = c->ncol - 2 * K;  // interior [K, ncol-K): needs nothing from the halo
-    auto interior = [&]() -> int {
-        if (ni <= 0) return IBLB_OK;
+    auto interior = [&](hipEvent_t stop) -> int {
+        if (ni <= 0) {
+            if (stop) HIP_TRY(c, hipEventRecord(stop, c->stream));
+            return IBLB_OK;
+        }
         Sweep2Args<T> a = sweep_args<T>(c, K, c->deep_balance ? 0 : W, c->ncol - K, (ni + W - 1) / W, W);
         a.vs = c->slab_vs;
         a.cus = c->ncu - c->reserved_cus;  // the compute stream's CU mask
+        if (!c->reserved_cus) a.spare = c->spare_slots;
         a.variant = c->deep_variant;
         size_t ev = 0;
         int r = ev_begin(c, &ev, c->stream);
         if (r) return r;
-        HIP_TRY(c, launch_sweepk<T>(a, K, false, c->stream));
+        HIP_TRY(c, launch_sweepk<T>(a, K, false, c->stream, stop));
         return ev_end(c, ev, EV_SWEEPK, (long long)ni * c->ny, c->stream);
     };
-    auto boundary = [&]() -> int {
+    auto boundary = [&](hipEvent_t stop) -> int {
         Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
         b.vs = c->slab_vs;
         b.variant = c->deep_variant;
-        HIP_TRY(c, launch_sweepk<T>(b, K, true, bs));
+        HIP_TRY(c, launch_sweepk<T>(b, K, true, bs, stop));
         return IBLB_OK;
     };
     if (!ov) {
-        if ((rc = exchange(c, bs, K)) || (rc = boundary()) || (rc = interior())) return rc;
+        if ((rc = exchange(c, bs, K)) || (rc = boundary(nullptr)) || (rc = interior(nullptr))) return rc;
         if ((rc = comm_follows(c))) return rc;
         c->deep_chain = false;
     } else {
+        // prev: the compute stream's work before interior(t) (interior(t-K) when chained)
+        hipEvent_t prev = c->ev_int, next = c->ev_int2;
         if (!(c->deep_chain && c->deep_chain_t == c->t && c->deep_chain_cur == c->cur))
-            HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
-        if ((rc = interior())) return rc;
-        if ((rc = comm_ready(c, K))) return rc;
+            HIP_TRY(c, hipEventRecord(prev, c->stream));
+        if ((rc = interior(next))) return rc;
+        if ((rc = comm_ready(c, K))) return rc;  // (waits for c->ev_int = prev)
         if ((rc = exchange(c, bs, K))) return rc;
-        HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
-        if ((rc = boundary())) return rc;
-        HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
-        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(bs, prev, 0));
+        if ((rc = boundary(c->ev_bnd))) return rc;
+        c->ev_int = next;
+        c->ev_int2 = prev;
         c->bnd_w = K;
         c->deep_chain = true;
     }
@@ -723,6 +730,7 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
         c->ncu = prop.multiProcessorCount;
         long reserve = 8;
+        c->spare_slots = 0;
         if (c->sweep_depth >= 3) {
             int nch = 0;
             const int wpc = is_f64(c) ? sweepk_geometry<double>(c->sweep_depth, c->slab_vs, c->deep_variant, true, c->ny, &nch)
@@ -731,6 +739,9 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
                 const long need = std::max(8L, (long)((2 * nch + wpc - 1) / wpc));
                 const long xcd = std::max(1, c->ncu / 8);
                 reserve = std::min((long)c->ncu / 2, (need + xcd - 1) / xcd * xcd);
+                // no reserved CUs: the interior's round leaves the boundary sweeps' waves (and a few
+                // for the RCCL kernels) free slots instead
+                c->spare_slots = 2 * nch + 16;
             }
         }
         reserve = env_long("IBLB_RESERVE_CUS", reserve);
@@ -761,7 +772,7 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         // cross-stream ordering events (producer and consumer on this device): no system-scope
         // fence (512 x 4096 self ring 0.0394 vs 0.0420 ms/iteration, profiles/r01u_gap_probe_event_fence.txt)
         const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
-        for (hipEvent_t* e : {&c->ev_bnd, &c->ev_int, &c->ev_pre, &c->ev_x, &c->ev_rccl})
+        for (hipEvent_t* e : {&c->ev_bnd, &c->ev_int, &c->ev_int2, &c->ev_pre, &c->ev_x, &c->ev_rccl})
             HIP_TRY(c, hipEventCreateWithFlags(e, evf));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));

@@ -312,12 +312,14 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->sweep_depth = (int)std::min(6L, std::max(2L, env_long("IBLB_SWEEP_DEPTH", 5)));
     c->deep_w = (int)env_long("IBLB_DEEP_W", f64 ? 96 : 64);
     c->deep_vs = (int)env_long("IBLB_DEEP_VS", 2);
-    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", 1);
+    // f32: the wall split (variant bit 1, three waves per SIMD: M f32 0.318 vs 0.341 ms per launch,
+    // profiles/r03sp)
+    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 1 : 3);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     // one cell per lane in a group slab's deep sweeps (self ring 512 / 1024 / 2048 x 4096: 0.0347 /
     // 0.0542 / 0.0935 ms/iteration vs 0.0380 / 0.0568 / 0.0942 with two, profiles/r01e7_*)
-    c->slab_vs = 1;
+    c->slab_vs = (int)env_long("IBLB_SLAB_VS", 1);
     // ghost columns: K for a deep cycle's halo, 3 for a one-step IB halo, 3K for the IB band
     // trapezoids that cross a slab edge (ctx_band.hip)
     c->gc = std::max(3, 3 * c->sweep_depth);
@@ -390,7 +392,7 @@ void iblb_destroy(iblb_ctx* c) {
     band_release(c);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
-    for (hipEvent_t e : {c->ev_bnd, c->ev_int, c->ev_pre, c->ev_x, c->ev_rccl})
+    for (hipEvent_t e : {c->ev_bnd, c->ev_int, c->ev_int2, c->ev_pre, c->ev_x, c->ev_rccl})
         if (e) (void)hipEventDestroy(e);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     void* bufs[] = {c->g_alloc, c->cil_samples, c->cil_lasts, c->cil_bpoints, c->rho0, c->u0, c->force0, c->d_s,

@@ -29,6 +29,10 @@
 // are the ghost columns of the buffer itself, filled by the halo exchange (whole columns, in place).
 #pragma once
 
+#include <hip/hip_ext.h>
+
+#include <cstdlib>
+
 #include "lbm_vec.h"
 
 namespace iblb {
@@ -640,24 +644,55 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
 template <int K, int VS>
 constexpr int ghost_lanes() { return (K - 1 + VS - 1) / VS; }
 
+// Wall split (WPE > 1, balanced sweeps only): the wall-row chunks — chunk 0 and the chunks from
+// a.wall_ch0 on — are walked by their own family of a.nsweep_w sweeps, listed after the
+// a.nsweep sweeps of the inner chunks [1, a.wall_ch0).  The kernel is built for WPE waves per SIMD
+// (f32: 3 instead of 2; the wall walk then spills a few VGPRs and is slower per column), and the
+// wall family's narrower sweeps let those waves finish with the others in the launch's one round.
+__device__ __forceinline__ void split_item(const int nin, const int nsw_in, const int nwall, int wv, int& sw, int& ch,
+                                           bool& wall) {
+    int b = (int)blockIdx.x;
+    const int q = (int)gridDim.x / 8;
+    if (b < 8 * q) b = (b % 8) * q + b / 8;
+    const int gw = b * 4 + wv;
+    const int ni = nsw_in * nin;
+    wall = gw >= ni;
+    if (!wall) {
+        sw = gw / nin;
+        ch = 1 + (gw - sw * nin);
+    } else {
+        const int g2 = gw - ni;
+        sw = g2 / nwall;
+        const int wc = g2 - sw * nwall;
+        ch = wc == 0 ? 0 : nin + wc;
+    }
+}
+
 // G ghost lanes at each wave edge (G * VS >= K - 1 rows)
-template <typename T, int VS, int MODE, int K, bool SLAB>
-__global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
+template <typename T, int VS, int MODE, int K, bool SLAB, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void sweepk_kernel(Sweep2Args<T> a) {
     constexpr int G = ghost_lanes<K, VS>();
     constexpr int OWN = 64 - 2 * G;  // owned lanes per wave
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int sw, ch;
-    linear_item(a.nch, wv, sw, ch);
-    if (sw >= a.nsweep || ch >= a.nch) return;
+    int sw, ch, nsw = a.nsweep;
+    if (WPE > 1) {
+        bool wall;
+        const int nin = a.wall_ch0 - 1;
+        split_item(nin, a.nsweep, a.nch - nin, wv, sw, ch, wall);
+        if (wall) nsw = a.nsweep_w;
+    } else {
+        linear_item(a.nch, wv, sw, ch);
+    }
+    if (sw >= nsw || ch >= a.nch) return;
     int xa, xb;
     if (a.col_step > 0) {
         xa = a.col_begin + sw * a.col_step;
         xb = min(xa + a.W, a.col_end);
-    } else {  // balanced: nsweep sweeps of floor/ceil((col_end - col_begin) / nsweep) columns
+    } else {  // balanced: nsw sweeps of floor/ceil((col_end - col_begin) / nsw) columns
         const long n = a.col_end - a.col_begin;
-        xa = a.col_begin + (int)(sw * n / a.nsweep);
-        xb = a.col_begin + (int)((sw + 1) * n / a.nsweep);
+        xa = a.col_begin + (int)(sw * n / nsw);
+        xb = a.col_begin + (int)((sw + 1) * n / nsw);
     }
     const int cs = ch * (OWN * VS);
     const int row0 = cs - G * VS;
@@ -682,62 +717,117 @@ __global__ __launch_bounds__(256) void sweepk_kernel(Sweep2Args<T> a) {
 }
 
 // Waves of one instantiation resident per CU (256-thread workgroups), and on `cus` CUs (0: all).
-template <typename T, int VS, int MODE, int K, bool SLAB>
+template <typename T, int VS, int MODE, int K, bool SLAB, int WPE>
 static long waves_per_cu() {
     static long cached = 0;
     if (cached) return cached;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweepk_kernel<T, VS, MODE, K, SLAB>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweepk_kernel<T, VS, MODE, K, SLAB, WPE>, 256, 0) !=
+            hipSuccess ||
         nb <= 0)
         return 0;
     cached = (long)nb * 4;
     return cached;
 }
-template <typename T, int VS, int MODE, int K, bool SLAB>
+template <typename T, int VS, int MODE, int K, bool SLAB, int WPE>
 static long resident_waves(int cus) {
     int dev = 0, ncu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
         return 0;
-    return waves_per_cu<T, VS, MODE, K, SLAB>() * (cus > 0 ? std::min(cus, ncu) : ncu);
+    return waves_per_cu<T, VS, MODE, K, SLAB, WPE>() * (cus > 0 ? std::min(cus, ncu) : ncu);
 }
 
-template <typename T, int VS, int MODE, int K, bool SLAB>
-static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s) {
+// wall split: sweeps of a wall-row chunk per sweep of an inner chunk, in quarters (the wall walk
+// of the 3-wave f32 build spills and runs slower per column)
+inline int wall_sweeps_x4() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("IBLB_DEEP_WALLX4");
+        v = e ? std::max(4, atoi(e)) : 8;
+    }
+    return v;
+}
+
+template <typename T, int VS, int MODE, int K, bool SLAB, int WPE>
+static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t stop) {
+    long waves;
     if (b.col_step <= 0) {
         // balanced sweeps: the wave count a whole number of device-wide rounds (the waves of one
         // launch all do the same work, so a partial last round idles the chip), sweeps close to
         // the requested W columns
         const long n = b.col_end - b.col_begin;
-        const long slots = resident_waves<T, VS, MODE, K, SLAB>(b.cus);
+        const long slots = std::max(0L, resident_waves<T, VS, MODE, K, SLAB, WPE>(b.cus) - b.spare);
         long ns = (n + b.W - 1) / b.W;
-        if (slots > 0) {
-            const long rounds = std::max(1L, (ns * b.nch + slots / 2) / slots);
-            ns = std::max(1L, rounds * slots / b.nch);
+        if (WPE > 1) {
+            // wall split: nin inner chunks with ns sweeps, nwall wall chunks with ns * r sweeps
+            const long nin = b.wall_ch0 - 1, nwall = b.nch - nin, r4 = wall_sweeps_x4();
+            if (slots > 0) {
+                const long rounds = std::max(1L, (ns * (4 * nin + r4 * nwall) / 4 + slots / 2) / slots);
+                ns = std::max(1L, 4 * rounds * slots / (4 * nin + r4 * nwall));
+            }
+            b.nsweep = (int)std::min(ns, n);
+            b.nsweep_w = (int)std::min((ns * r4 + 3) / 4, n);
+            waves = (long)b.nsweep * nin + (long)b.nsweep_w * nwall;
+        } else {
+            if (slots > 0) {
+                const long rounds = std::max(1L, (ns * b.nch + slots / 2) / slots);
+                ns = std::max(1L, rounds * slots / b.nch);
+            }
+            b.nsweep = (int)std::min(ns, n);
+            waves = (long)b.nsweep * b.nch;
         }
-        b.nsweep = (int)std::min(ns, n);
+    } else {
+        if (WPE > 1) return hipErrorInvalidValue;  // the split needs balanced sweeps
+        waves = (long)b.nsweep * b.nch;
     }
-    const unsigned blocks = (unsigned)(((long)b.nsweep * b.nch + 3) / 4);
-    sweepk_kernel<T, VS, MODE, K, SLAB><<<blocks, 256, 0, s>>>(b);
+    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    if (stop)  // the event rides on the kernel's own completion signal: no marker packet after it
+        hipExtLaunchKernelGGL(sweepk_kernel<T, VS, MODE, K, SLAB, WPE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, b);
+    else
+        sweepk_kernel<T, VS, MODE, K, SLAB, WPE><<<blocks, 256, 0, s>>>(b);
     return hipGetLastError();
 }
 
+// the first chunk after chunk 0 whose wave holds a wall row (ghost lanes included), as the kernel
+// decides it (row0 <= 0 || row0 + 64 VS >= ny)
+template <int K, int VS>
+inline int first_wall_chunk(int ny, int nch) {
+    constexpr int G = ghost_lanes<K, VS>();
+    for (int ch = 1; ch < nch; ++ch)
+        if (ch * (64 - 2 * G) * VS - G * VS + 64 * VS >= ny) return ch;
+    return nch;
+}
+
+// the f32 wall split (variant bit 1): two cells per lane, three waves per SIMD
+template <typename T, int VS>
+constexpr bool wall_split_built() { return sizeof(T) == 4 && VS == 2; }
+
 template <typename T, int VS, int K, bool SLAB>
-static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s) {
+static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEvent_t stop) {
     constexpr int G = ghost_lanes<K, VS>();
     const int rows_per_wave = (64 - 2 * G) * VS;  // owned rows
     Sweep2Args<T> b = a;
     b.nch = (a.L.ny + rows_per_wave - 1) / rows_per_wave;
-    // variants: 1 = nontemporal stores (default), 0 = plain
-    if (a.variant == 0) return launch_sweepk_mode<T, VS, 0, K, SLAB>(b, s);
-    return launch_sweepk_mode<T, VS, 1, K, SLAB>(b, s);
+    if constexpr (wall_split_built<T, VS>()) {
+        if ((a.variant & 2) && a.col_step <= 0) {
+            b.wall_ch0 = first_wall_chunk<K, VS>(a.L.ny, b.nch);
+            if (b.wall_ch0 >= 2) {
+                if (a.variant & 1) return launch_sweepk_mode<T, VS, 1, K, SLAB, 3>(b, s, stop);
+                return launch_sweepk_mode<T, VS, 0, K, SLAB, 3>(b, s, stop);
+            }
+        }
+    }
+    // variants: bit 0 = nontemporal stores (default), 0 = plain
+    if (a.variant & 1) return launch_sweepk_mode<T, VS, 1, K, SLAB, 1>(b, s, stop);
+    return launch_sweepk_mode<T, VS, 0, K, SLAB, 1>(b, s, stop);
 }
 
 // cells per lane: 2 or 1 (4 in f32 measured slower: one wave per SIMD, profiles/r01d4_*)
 template <typename T, int K, bool SLAB>
-hipError_t launch_sweepk_depth(const Sweep2Args<T>& a, hipStream_t s) {
-    if (a.vs == 2) return launch_sweepk_vs<T, 2, K, SLAB>(a, s);
-    if (a.vs == 1) return launch_sweepk_vs<T, 1, K, SLAB>(a, s);
+hipError_t launch_sweepk_depth(const Sweep2Args<T>& a, hipStream_t s, hipEvent_t stop) {
+    if (a.vs == 2) return launch_sweepk_vs<T, 2, K, SLAB>(a, s, stop);
+    if (a.vs == 1) return launch_sweepk_vs<T, 1, K, SLAB>(a, s, stop);
     return hipErrorInvalidValue;
 }
 
@@ -748,10 +838,10 @@ template <typename T, int K, bool SLAB>
 int deep_geometry(int vs, int variant, int ny, int* nch) {
     if (vs == 2) {
         *nch = (ny + (64 - 2 * ghost_lanes<K, 2>()) * 2 - 1) / ((64 - 2 * ghost_lanes<K, 2>()) * 2);
-        return (int)(variant == 0 ? waves_per_cu<T, 2, 0, K, SLAB>() : waves_per_cu<T, 2, 1, K, SLAB>());
+        return (int)((variant & 1) ? waves_per_cu<T, 2, 1, K, SLAB, 1>() : waves_per_cu<T, 2, 0, K, SLAB, 1>());
     }
     *nch = (ny + (64 - 2 * ghost_lanes<K, 1>()) - 1) / (64 - 2 * ghost_lanes<K, 1>());
-    return (int)(variant == 0 ? waves_per_cu<T, 1, 0, K, SLAB>() : waves_per_cu<T, 1, 1, K, SLAB>());
+    return (int)((variant & 1) ? waves_per_cu<T, 1, 1, K, SLAB, 1>() : waves_per_cu<T, 1, 0, K, SLAB, 1>());
 }
 
 }  // namespace iblb
