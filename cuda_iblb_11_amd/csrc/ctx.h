@@ -75,7 +75,6 @@ struct iblb_ctx {
     int deep_w = 96, deep_vs = 2, deep_variant = 1, deep_balance = 1;  // IBLB_DEEP_W / _VS / _VARIANT / _BALANCE
     int slab_vs = 1;            // cells per lane of a group slab's deep sweeps
     int reserved_cus = 0, ncu = 0;  // CUs kept free of the compute stream (RCCL groups), device CUs
-    int spare_slots = 0;            // without reserved CUs: wave slots the interior sweeps leave free
     std::vector<uint32_t> comp_mask;  // the compute stream's CU mask when reserved_cus > 0
     hipStream_t stream = nullptr;
     iblb::Coef coef{};
@@ -279,6 +278,10 @@ Halo<T> halo_of(iblb_ctx* c, int which) {
 // ---- profiling (iblb_ctx.hip) ----
 int ev_begin(iblb_ctx* c, size_t* idx, hipStream_t st = nullptr);
 int ev_end(iblb_ctx* c, size_t idx, int kind, long long cells = 0, hipStream_t st = nullptr);
+// timing events that a launch carries itself (hipExtLaunchKernelGGL start / stop: the kernel's own
+// dispatch and completion signals, no marker packets); null when not profiling
+int ev_kernel(iblb_ctx* c, size_t* idx, hipEvent_t* start, hipEvent_t* stop);
+int ev_kernel_end(iblb_ctx* c, size_t idx, int kind, long long cells);
 
 // ---- halo / force (ctx_step.hip) ----
 int rccl_order(iblb_ctx* c, hipStream_t st);

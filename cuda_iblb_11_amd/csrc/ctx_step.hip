@@ -339,10 +339,11 @@ static int sweepk_step(iblb_ctx* c) {
     a.vs = c->deep_vs;
     a.variant = c->deep_variant;
     size_t ev = 0;
-    int rc = ev_begin(c, &ev, c->stream);
+    hipEvent_t e0, e1;  // timing on the launch's own signals (profiling only)
+    int rc = ev_kernel(c, &ev, &e0, &e1);
     if (rc) return rc;
-    HIP_TRY(c, launch_sweepk<T>(a, c->sweep_depth, false, c->stream));
-    if ((rc = ev_end(c, ev, EV_SWEEPK, (long long)c->ncol * c->ny, c->stream))) return rc;
+    HIP_TRY(c, launch_sweepk<T>(a, c->sweep_depth, false, c->stream, e1, e0));
+    if ((rc = ev_kernel_end(c, ev, EV_SWEEPK, (long long)c->ncol * c->ny))) return rc;
     after_sweep(c, c->sweep_depth);
     return IBLB_OK;
 }
@@ -376,7 +377,6 @@ static int deep_slab_step(iblb_ctx* c) {
         Sweep2Args<T> a = sweep_args<T>(c, K, c->deep_balance ? 0 : W, c->ncol - K, (ni + W - 1) / W, W);
         a.vs = c->slab_vs;
         a.cus = c->ncu - c->reserved_cus;  // the compute stream's CU mask
-        if (!c->reserved_cus) a.spare = c->spare_slots;
         a.variant = c->deep_variant;
         size_t ev = 0;
         int r = ev_begin(c, &ev, c->stream);
@@ -730,7 +730,6 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
         c->ncu = prop.multiProcessorCount;
         long reserve = 8;
-        c->spare_slots = 0;
         if (c->sweep_depth >= 3) {
             int nch = 0;
             const int wpc = is_f64(c) ? sweepk_geometry<double>(c->sweep_depth, c->slab_vs, c->deep_variant, true, c->ny, &nch)
@@ -739,9 +738,6 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
                 const long need = std::max(8L, (long)((2 * nch + wpc - 1) / wpc));
                 const long xcd = std::max(1, c->ncu / 8);
                 reserve = std::min((long)c->ncu / 2, (need + xcd - 1) / xcd * xcd);
-                // no reserved CUs: the interior's round leaves the boundary sweeps' waves (and a few
-                // for the RCCL kernels) free slots instead
-                c->spare_slots = 2 * nch + 16;
             }
         }
         reserve = env_long("IBLB_RESERVE_CUS", reserve);

@@ -47,8 +47,7 @@ static int ev_drain(iblb_ctx* c) {
     return IBLB_OK;
 }
 
-int ev_begin(iblb_ctx* c, size_t* idx, hipStream_t st) {
-    if (!c->prof) return IBLB_OK;
+static int ev_reserve(iblb_ctx* c, size_t* idx) {
     if (c->ev_used + 2 > c->ev_pool.size()) {
         // timing events bracket kernels of this device only: no system-scope fence
         for (int k = 0; k < 64; ++k) {
@@ -59,21 +58,47 @@ int ev_begin(iblb_ctx* c, size_t* idx, hipStream_t st) {
     }
     *idx = c->ev_used;
     c->ev_used += 2;
+    return IBLB_OK;
+}
+
+int ev_begin(iblb_ctx* c, size_t* idx, hipStream_t st) {
+    if (!c->prof) return IBLB_OK;
+    int rc = ev_reserve(c, idx);
+    if (rc) return rc;
     HIP_TRY(c, hipEventRecord(c->ev_pool[*idx], st ? st : c->stream));
+    return IBLB_OK;
+}
+
+static int ev_note(iblb_ctx* c, size_t idx, int kind, long long cells) {
+    c->ev_kind.push_back({kind, idx, cells});
+    if (c->ev_used >= 8192) {  // bound the pool: drain what is recorded
+        HIP_TRY(c, hipEventSynchronize(c->ev_pool[idx + 1]));
+        for (hipStream_t s : {c->stream, c->comm_stream, c->band_st, c->deep_st})
+            if (s) HIP_TRY(c, hipStreamSynchronize(s));
+        return ev_drain(c);
+    }
     return IBLB_OK;
 }
 
 int ev_end(iblb_ctx* c, size_t idx, int kind, long long cells, hipStream_t st) {
     if (!c->prof) return IBLB_OK;
     HIP_TRY(c, hipEventRecord(c->ev_pool[idx + 1], st ? st : c->stream));
-    c->ev_kind.push_back({kind, idx, cells});
-    if (c->ev_used >= 8192) {  // bound the pool: drain what is recorded
-        HIP_TRY(c, hipEventSynchronize(c->ev_pool[idx + 1]));
-        for (hipStream_t s : {c->comm_stream, c->band_st, c->deep_st})
-            if (s) HIP_TRY(c, hipStreamSynchronize(s));
-        return ev_drain(c);
-    }
+    return ev_note(c, idx, kind, cells);
+}
+
+int ev_kernel(iblb_ctx* c, size_t* idx, hipEvent_t* start, hipEvent_t* stop) {
+    *start = *stop = nullptr;
+    if (!c->prof) return IBLB_OK;
+    int rc = ev_reserve(c, idx);
+    if (rc) return rc;
+    *start = c->ev_pool[*idx];
+    *stop = c->ev_pool[*idx + 1];
     return IBLB_OK;
+}
+
+int ev_kernel_end(iblb_ctx* c, size_t idx, int kind, long long cells) {
+    if (!c->prof) return IBLB_OK;
+    return ev_note(c, idx, kind, cells);
 }
 
 // ---- allocation ---------------------------------------------------------------------------------
@@ -319,7 +344,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     // one cell per lane in a group slab's deep sweeps (self ring 512 / 1024 / 2048 x 4096: 0.0347 /
     // 0.0542 / 0.0935 ms/iteration vs 0.0380 / 0.0568 / 0.0942 with two, profiles/r01e7_*)
-    c->slab_vs = (int)env_long("IBLB_SLAB_VS", 1);
+    c->slab_vs = 1;
     // ghost columns: K for a deep cycle's halo, 3 for a one-step IB halo, 3K for the IB band
     // trapezoids that cross a slab edge (ctx_band.hip)
     c->gc = std::max(3, 3 * c->sweep_depth);

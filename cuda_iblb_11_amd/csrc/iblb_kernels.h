@@ -62,7 +62,6 @@ struct Sweep2Args {
     int nsweep_w = 0;    // wall split (set by the launcher): sweeps of the wall-row chunks,
     int wall_ch0 = 0;    // and the first wall-row chunk after chunk 0
     int cus;             // deep sweeps, balanced widths: CUs the launch's stream may use (0 = all)
-    int spare = 0;       // ... and wave slots on them left to other streams' kernels
     int flux_col;        // local column sampled for Q (every iteration), or -1
     int fskip0, fskip1;  // rows [fskip0, fskip1) of the flux column are not sampled (an IB band
                          // patch covers them: its trapezoid's last level adds their flux)
@@ -79,9 +78,10 @@ template <typename T>
 hipError_t launch_sweep2(Sweep2Args<T> a, bool ghost, hipStream_t s);
 // K = depth (3 .. 6) iterations per launch: g^t -> g^{t+K}; ghost as above (a
 // boundary sweep of output columns [0, K) reads columns -K .. 2K-1).  col_step 0: balanced widths.
-// stop: recorded by the kernel's completion signal (no marker packet)
+// start / stop: recorded by the kernel's dispatch / completion signals (no marker packets)
 template <typename T>
-hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool ghost, hipStream_t s, hipEvent_t stop = nullptr);
+hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool ghost, hipStream_t s, hipEvent_t stop = nullptr,
+                         hipEvent_t start = nullptr);
 // Resident waves per CU of a deep-sweep configuration; *nch = its row chunks for ny rows.
 template <typename T>
 int sweepk_geometry(int depth, int vs, int variant, bool ghost, int ny, int* nch);

@@ -6,7 +6,7 @@ namespace iblb {
 
 // the K-iteration kernels are built in lbm_sweepk<K>.hip
 #define IBLB_SWEEPK_EXTERN(T, K, S)                                                          \
-    extern template hipError_t launch_sweepk_depth<T, K, S>(const Sweep2Args<T>&, hipStream_t, hipEvent_t); \
+    extern template hipError_t launch_sweepk_depth<T, K, S>(const Sweep2Args<T>&, hipStream_t, hipEvent_t, hipEvent_t); \
     extern template int deep_geometry<T, K, S>(int, int, int, int*);
 #define IBLB_SWEEPK_EXTERN_K(K)                                                                               \
     IBLB_SWEEPK_EXTERN(double, K, false) IBLB_SWEEPK_EXTERN(double, K, true) IBLB_SWEEPK_EXTERN(float, K, false) \
@@ -17,11 +17,12 @@ IBLB_SWEEPK_EXTERN_K(5)
 IBLB_SWEEPK_EXTERN_K(6)
 
 template <typename T, bool SLAB>
-static hipError_t launch_sweepk_slab(const Sweep2Args<T>& a, int depth, hipStream_t s, hipEvent_t stop) {
-    if (depth == 3) return launch_sweepk_depth<T, 3, SLAB>(a, s, stop);
-    if (depth == 4) return launch_sweepk_depth<T, 4, SLAB>(a, s, stop);
-    if (depth == 5) return launch_sweepk_depth<T, 5, SLAB>(a, s, stop);
-    if (depth == 6) return launch_sweepk_depth<T, 6, SLAB>(a, s, stop);
+static hipError_t launch_sweepk_slab(const Sweep2Args<T>& a, int depth, hipStream_t s, hipEvent_t stop,
+                                     hipEvent_t start) {
+    if (depth == 3) return launch_sweepk_depth<T, 3, SLAB>(a, s, stop, start);
+    if (depth == 4) return launch_sweepk_depth<T, 4, SLAB>(a, s, stop, start);
+    if (depth == 5) return launch_sweepk_depth<T, 5, SLAB>(a, s, stop, start);
+    if (depth == 6) return launch_sweepk_depth<T, 6, SLAB>(a, s, stop, start);
     return hipErrorInvalidValue;
 }
 
@@ -42,19 +43,20 @@ template int sweepk_geometry<double>(int, int, int, bool, int, int*);
 template int sweepk_geometry<float>(int, int, int, bool, int, int*);
 
 template <typename T>
-hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool slab, hipStream_t s, hipEvent_t stop) {
+hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool slab, hipStream_t s, hipEvent_t stop, hipEvent_t start) {
     if (a.nsweep <= 0) return hipSuccess;
     // rows are read from row0 - 1 >= -(K-1) - VS - 1 to the last wave's row0 + 64*VS: inside the
     // 512-element guards of the buffers
     if (a.W <= 0 || a.L.ncol < 1 || a.vs <= 0 || a.L.rows % a.vs != 0 || a.L.plane % a.vs != 0 ||
         a.L.col % a.vs != 0)
         return hipErrorInvalidValue;
-    return slab ? launch_sweepk_slab<T, true>(a, depth, s, stop) : launch_sweepk_slab<T, false>(a, depth, s, stop);
+    return slab ? launch_sweepk_slab<T, true>(a, depth, s, stop, start)
+                : launch_sweepk_slab<T, false>(a, depth, s, stop, start);
 }
 
 template hipError_t launch_sweep2<double>(Sweep2Args<double>, bool, hipStream_t);
 template hipError_t launch_sweep2<float>(Sweep2Args<float>, bool, hipStream_t);
-template hipError_t launch_sweepk<double>(Sweep2Args<double>, int, bool, hipStream_t, hipEvent_t);
-template hipError_t launch_sweepk<float>(Sweep2Args<float>, int, bool, hipStream_t, hipEvent_t);
+template hipError_t launch_sweepk<double>(Sweep2Args<double>, int, bool, hipStream_t, hipEvent_t, hipEvent_t);
+template hipError_t launch_sweepk<float>(Sweep2Args<float>, int, bool, hipStream_t, hipEvent_t, hipEvent_t);
 
 }  // namespace iblb

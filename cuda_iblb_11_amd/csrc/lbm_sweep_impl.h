@@ -31,8 +31,6 @@
 
 #include <hip/hip_ext.h>
 
-#include <cstdlib>
-
 #include "lbm_vec.h"
 
 namespace iblb {
@@ -739,29 +737,23 @@ static long resident_waves(int cus) {
 }
 
 // wall split: sweeps of a wall-row chunk per sweep of an inner chunk, in quarters (the wall walk
-// of the 3-wave f32 build spills and runs slower per column)
-inline int wall_sweeps_x4() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("IBLB_DEEP_WALLX4");
-        v = e ? std::max(4, atoi(e)) : 8;
-    }
-    return v;
-}
+// of the 3-wave f32 build spills and runs ~1.4x slower per column; M f32 per launch with 1, 1.5, 2,
+// 2.25, 2.5, 3: 0.455, 0.370, 0.305-0.320, 0.329, 0.314, 0.326 ms, profiles/r03sp, r03r2)
+constexpr int WALL_SWEEPS_X4 = 8;
 
 template <typename T, int VS, int MODE, int K, bool SLAB, int WPE>
-static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t stop) {
+static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t stop, hipEvent_t start) {
     long waves;
     if (b.col_step <= 0) {
         // balanced sweeps: the wave count a whole number of device-wide rounds (the waves of one
         // launch all do the same work, so a partial last round idles the chip), sweeps close to
         // the requested W columns
         const long n = b.col_end - b.col_begin;
-        const long slots = std::max(0L, resident_waves<T, VS, MODE, K, SLAB, WPE>(b.cus) - b.spare);
+        const long slots = resident_waves<T, VS, MODE, K, SLAB, WPE>(b.cus);
         long ns = (n + b.W - 1) / b.W;
         if (WPE > 1) {
             // wall split: nin inner chunks with ns sweeps, nwall wall chunks with ns * r sweeps
-            const long nin = b.wall_ch0 - 1, nwall = b.nch - nin, r4 = wall_sweeps_x4();
+            const long nin = b.wall_ch0 - 1, nwall = b.nch - nin, r4 = WALL_SWEEPS_X4;
             if (slots > 0) {
                 const long rounds = std::max(1L, (ns * (4 * nin + r4 * nwall) / 4 + slots / 2) / slots);
                 ns = std::max(1L, 4 * rounds * slots / (4 * nin + r4 * nwall));
@@ -782,8 +774,8 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
         waves = (long)b.nsweep * b.nch;
     }
     const unsigned blocks = (unsigned)((waves + 3) / 4);
-    if (stop)  // the event rides on the kernel's own completion signal: no marker packet after it
-        hipExtLaunchKernelGGL(sweepk_kernel<T, VS, MODE, K, SLAB, WPE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, b);
+    if (stop || start)  // the events ride on the kernel's own signals: no marker packets around it
+        hipExtLaunchKernelGGL(sweepk_kernel<T, VS, MODE, K, SLAB, WPE>, dim3(blocks), dim3(256), 0, s, start, stop, 0, b);
     else
         sweepk_kernel<T, VS, MODE, K, SLAB, WPE><<<blocks, 256, 0, s>>>(b);
     return hipGetLastError();
@@ -804,7 +796,7 @@ template <typename T, int VS>
 constexpr bool wall_split_built() { return sizeof(T) == 4 && VS == 2; }
 
 template <typename T, int VS, int K, bool SLAB>
-static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEvent_t stop) {
+static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEvent_t stop, hipEvent_t start) {
     constexpr int G = ghost_lanes<K, VS>();
     const int rows_per_wave = (64 - 2 * G) * VS;  // owned rows
     Sweep2Args<T> b = a;
@@ -813,21 +805,21 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
         if ((a.variant & 2) && a.col_step <= 0) {
             b.wall_ch0 = first_wall_chunk<K, VS>(a.L.ny, b.nch);
             if (b.wall_ch0 >= 2) {
-                if (a.variant & 1) return launch_sweepk_mode<T, VS, 1, K, SLAB, 3>(b, s, stop);
-                return launch_sweepk_mode<T, VS, 0, K, SLAB, 3>(b, s, stop);
+                if (a.variant & 1) return launch_sweepk_mode<T, VS, 1, K, SLAB, 3>(b, s, stop, start);
+                return launch_sweepk_mode<T, VS, 0, K, SLAB, 3>(b, s, stop, start);
             }
         }
     }
     // variants: bit 0 = nontemporal stores (default), 0 = plain
-    if (a.variant & 1) return launch_sweepk_mode<T, VS, 1, K, SLAB, 1>(b, s, stop);
-    return launch_sweepk_mode<T, VS, 0, K, SLAB, 1>(b, s, stop);
+    if (a.variant & 1) return launch_sweepk_mode<T, VS, 1, K, SLAB, 1>(b, s, stop, start);
+    return launch_sweepk_mode<T, VS, 0, K, SLAB, 1>(b, s, stop, start);
 }
 
 // cells per lane: 2 or 1 (4 in f32 measured slower: one wave per SIMD, profiles/r01d4_*)
 template <typename T, int K, bool SLAB>
-hipError_t launch_sweepk_depth(const Sweep2Args<T>& a, hipStream_t s, hipEvent_t stop) {
-    if (a.vs == 2) return launch_sweepk_vs<T, 2, K, SLAB>(a, s, stop);
-    if (a.vs == 1) return launch_sweepk_vs<T, 1, K, SLAB>(a, s, stop);
+hipError_t launch_sweepk_depth(const Sweep2Args<T>& a, hipStream_t s, hipEvent_t stop, hipEvent_t start) {
+    if (a.vs == 2) return launch_sweepk_vs<T, 2, K, SLAB>(a, s, stop, start);
+    if (a.vs == 1) return launch_sweepk_vs<T, 1, K, SLAB>(a, s, stop, start);
     return hipErrorInvalidValue;
 }
 

@@ -5,7 +5,7 @@
 namespace iblb {
 
 #define IBLB_SWEEPK_INST(T, S)                                                               \
-    template hipError_t launch_sweepk_depth<T, 6, S>(const Sweep2Args<T>&, hipStream_t, hipEvent_t); \
+    template hipError_t launch_sweepk_depth<T, 6, S>(const Sweep2Args<T>&, hipStream_t, hipEvent_t, hipEvent_t); \
     template int deep_geometry<T, 6, S>(int, int, int, int*);
 IBLB_SWEEPK_INST(double, false)
 IBLB_SWEEPK_INST(double, true)

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (IBLB_DEEP_WALLX4, IBLB_SLAB_VS and the spare-slot sizing were temporary experiment hooks, removed after these runs)
 # (1) f32 wall split: wall sweeps per inner sweep (IBLB_DEEP_WALLX4 / 4) around the optimum;
 # (2) strong-scaling slabs on the RCCL self ring: reserved CUs (default) vs none with spare wave
 #     slots (IBLB_RESERVE_CUS=0), one vs two cells per lane in the slab sweeps (IBLB_SLAB_VS).

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (IBLB_DEEP_WALLX4, IBLB_SLAB_VS and the spare-slot sizing were temporary experiment hooks, removed after these runs)
 # f32 deep sweep, wall split (IBLB_DEEP_VARIANT bit 1: the three-wave build, the wall-row chunks as
 # their own sweep family): bit-identity tests, then M f32 / K5 benches alternating the default
 # variant (1) and the split (3) with wall sweeps per inner sweep IBLB_DEEP_WALLX4 / 4.
