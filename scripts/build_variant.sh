@@ -5,7 +5,7 @@
 # replaced .hip are rebuilt, the other objects come from cuda_iblb_11_amd/build.
 set -e
 name=$1; dir=$2; shift 2
-out=cuda_iblb_11_amd/lib/variants; tmp=/tmp/var_$name
+out=cuda_iblb_11_amd/lib/variants; tmp=cuda_iblb_11_amd/vbuild_$name  # csrc depth: ctx.h includes ../../include
 rm -rf $tmp; mkdir -p $out $tmp
 cp cuda_iblb_11_amd/csrc/*.h cuda_iblb_11_amd/csrc/*.hip $tmp/
 cp $dir/* $tmp/ 2>/dev/null || true
