@@ -139,6 +139,13 @@ struct iblb_ctx {
     hipEvent_t band_end = nullptr; // recorded on the deep stream at the end of the last band cycle
     char* s_alloc = nullptr;     // two scratch population buffers of the trapezoid (layout of g)
     void* sbuf[2] = {nullptr, nullptr};
+    int band_merge = 1;          // IBLB_BAND_MERGE: 1 auto, 2 always, 0 never: each level's launch also
+                                 // evaluates the next level's force (merged chain)
+    bool band_merged = false;    // the installed plan runs the merged chain
+    double* bf_alloc = nullptr;  // merged chain: two more dense force buffers (levels j % 3 = 1, 2) ...
+    uint8_t* bfl_alloc = nullptr;  // ... and their chunk flags (zero between cycles)
+    double* bfd[2] = {nullptr, nullptr};
+    uint8_t* bfl[2] = {nullptr, nullptr};
     int band_reserve = 0;        // CUs of the band chain's stream (0: one stream, in sequence; -2: unmasked)
     bool band_sticky = false;    // keep the streams while a schedule runs
     hipStream_t band_st = nullptr;  // the band chain (masked to the reserved CUs)

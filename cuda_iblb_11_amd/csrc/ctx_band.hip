@@ -255,6 +255,24 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     if (!tab.empty()) std::memcpy(c->band_pin[slot], tab.data(), tab.size() * sizeof(int));
     c->band_tab = c->band_pin[slot];
     c->band_pin_cur = slot;
+    // merged chain (IBLB_BAND_MERGE 1 = auto): where the chain, not the deep sweep beside it, is the
+    // cycle's critical path (the deep sweep shorter than 1.5x a chain of 2K ~8 us launches: narrow
+    // slabs).  Its launches are longer than the one-step launches they replace (the point groups
+    // recompute the level's collide over their nodes' pulls): beside a long deep sweep it only adds
+    // work (K3 0.0378 vs 0.0359 ms/iteration); on the K5-width slab it saves 3-6 % (profiles/r03mg)
+    {
+        const double deep_us = (double)K * deep_cols * ny / (is_f64(c) ? 130e3 : 190e3);
+        c->band_merged = c->band_merge == 2 || (c->band_merge == 1 && deep_us < 1.5 * 2 * K * 8.0);
+    }
+    if (c->band_merged && !c->bf_alloc) {  // merged chain: the force buffers of levels j % 3 = 1, 2
+        const size_t width = (size_t)c->ncol + 2 * c->gc;
+        if ((rc = alloc_zero(c, (void**)&c->bf_alloc, 4 * (size_t)c->fplane * sizeof(double)))) return rc;
+        if ((rc = alloc_zero(c, (void**)&c->bfl_alloc, 2 * width * c->nch))) return rc;
+        for (int i = 0; i < 2; ++i) {
+            c->bfd[i] = c->bf_alloc + (size_t)i * 2 * c->fplane + (long)c->gc * c->L.rows;
+            c->bfl[i] = c->bfl_alloc + (size_t)i * width * c->nch + (long)c->gc * c->nch;
+        }
+    }
     if (!c->s_alloc) {  // the trapezoid's scratch levels: two buffers laid out like g
         const size_t bytes = (size_t)(2 * c->buf_elems + 2 * GUARD) * c->esize;
         if ((rc = alloc_zero(c, (void**)&c->s_alloc, bytes))) return rc;
@@ -337,40 +355,73 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     return ev_end(c, ev, EV_SWEEPK, (long long)n * c->ny, ds);
 }
 
-// The band chain as 2K dependent launches on bs: the IB of each level over every point (image)
-// forcing the columns the level computes, then the level's one-step launch over the trapezoid's
-// entries; the deep sweep on ds; the last level after the deep sweep (on ds, right behind it) and,
-// when it stores a slab's edge columns, after the boundary sweeps (ev_bnd).  c->band_end is
-// recorded on ds at the end (by the last level's own completion where it launches).
+// Columns the force of level j may be spread into (the band trapezoid's [clo, chi)).  Chained
+// levels: the columns level j computes; the last level stores the slab's own columns only, so a
+// force left in a ghost column would never be consumed.  Merged chain: one column less at each
+// ghost edge (the launch after a level clears that level's force at its own entries, one column
+// narrower: the dropped column lies inside the garbage frontier, at level j columns up to
+// -D+2+3j are garbage, §5 of DESIGN.md), and level K-2 only where the last level's cells and the
+// nodes of its force pull: columns -3 .. ncol+2 (a point forcing column 0 has nodes from -1, their
+// pulls from -2, the collides of those from -3); the last launch clears those outside its own.
+static void force_clip(const iblb_ctx* c, int j, bool merged, int* clo, int* chi) {
+    const int K = c->sweep_depth, D = c->band_d, n = c->ncol;
+    if (j == K - 1) {
+        *clo = std::max(0, -D + 1 + j);
+        *chi = std::min(n, n + D - 1 - j);
+    } else if (!merged) {
+        *clo = -D + 1 + j;
+        *chi = n + D - 1 - j;
+    } else if (j == K - 2) {
+        *clo = std::max(-3, -D + 2 + j);
+        *chi = std::min(n + 3, n + D - 2 - j);
+    } else {
+        *clo = -D + 2 + j;
+        *chi = n + D - 2 - j;
+    }
+}
+
+// The band chain on bs.  Chained (IBLB_BAND_MERGE=0): 2K dependent launches, the IB of each level
+// over every point (image) forcing the columns the level computes, then the level's one-step
+// launch over the trapezoid's entries.  Merged (default): K launches, level j's launch also
+// evaluating level j+1's force (band_level_kernel: its point groups recompute level j's collide
+// over their nodes' pulls), into three force buffers used in turn (level j: j % 3; the main dense
+// force is buffer 0); level j's force is read, not consumed, by its launch (the point groups read it
+// too) and cleared by the next launch.  The deep sweep on ds; the last level after the deep sweep
+// (on ds, right behind it) and, when it stores a slab's edge columns, after the boundary sweeps
+// (ev_bnd).  c->band_end is recorded on ds at the end (by the last level's own completion where it
+// launches).
 template <typename T>
 static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool slab, hipStream_t bs, hipStream_t ds) {
     int rc;
     const int D = c->band_d;
+    const bool merged = c->band_merged && c->bf_alloc;
+    double* fd[3] = {c->fdense, c->bfd[0], c->bfd[1]};
+    uint8_t* fl[3] = {c->flags, c->bfl[0], c->bfl[1]};
+    int clo0, chi0;
+    force_clip(c, 0, merged, &clo0, &chi0);
     if (c->ib_state == IB_PENDING) {  // force^t from g^t
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, bs))) return rc;
-        if ((rc = ib_ghost(c, A, D, -D + 1, c->ncol + D - 1, pts_s(c), pts_us(c), pts_eps(c), 0, bs))) return rc;
+        if ((rc = ib_ghost(c, A, D, clo0, chi0, pts_s(c), pts_us(c), pts_eps(c), 0, bs))) return rc;
         if ((rc = ev_end(c, ev, EV_IB, 0, bs))) return rc;
         c->ib_state = IB_READY;
     } else if (D > 0) {
         // force^t was evaluated before the cycle (a reader, new points, a one-step iteration) for the
         // slab's own columns only: level 0 of the ghost trapezoids needs it in the ghost columns too
-        if ((rc = ib_ghost(c, A, D, -D + 1, 0, pts_s(c), pts_us(c), pts_eps(c), 0, bs))) return rc;
-        if ((rc = ib_ghost(c, A, D, c->ncol, c->ncol + D - 1, pts_s(c), pts_us(c), pts_eps(c), 0, bs))) return rc;
+        if ((rc = ib_ghost(c, A, D, clo0, 0, pts_s(c), pts_us(c), pts_eps(c), 0, bs))) return rc;
+        if ((rc = ib_ghost(c, A, D, c->ncol, chi0, pts_s(c), pts_us(c), pts_eps(c), 0, bs))) return rc;
     }
     // the deep sweep first: the chip is full while it runs
     if ((rc = band_deep<T>(c, K, ds))) return rc;
     for (int j = 0; j < K; ++j) {
         const T* src = j == 0 ? A : S[(j - 1) & 1];
         T* dst = j == K - 1 ? B : S[j & 1];
-        if (j > 0) {  // force^{t+j} from the level below, with the points of iteration t+j-1
+        if (j > 0 && !merged) {  // force^{t+j} from the level below, with the points of iteration t+j-1
             const float *ps, *pus;
             const int* pe;
             pts_of(c, c->t + j - 1, &ps, &pus, &pe);
-            // force into the columns level j computes; the last level stores the slab's own
-            // columns only, so a force left in a ghost column would never be consumed
-            const int clo = j == K - 1 ? std::max(0, -D + 1 + j) : -D + 1 + j;
-            const int chi = j == K - 1 ? std::min(c->ncol, c->ncol + D - 1 - j) : c->ncol + D - 1 - j;
+            int clo, chi;
+            force_clip(c, j, false, &clo, &chi);
             size_t ev = 0;
             if ((rc = ev_begin(c, &ev, bs))) return rc;
             if ((rc = ib_ghost(c, src, D, clo, chi, ps, pus, pe, 0, bs))) return rc;
@@ -389,8 +440,8 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
         a.row_tab = 1;
         a.nchl = c->band_nchl[j];
         a.store_rows = j == K - 1;  // the last level writes g^{t+K}: patch output rows only
-        a.flags = c->flags;
-        a.fdense = c->fdense;
+        a.flags = merged ? fl[j % 3] : c->flags;
+        a.fdense = merged ? fd[j % 3] : c->fdense;
         a.fplane = c->fplane;
         a.flux_col = c->band_flux;  // rows [fy0, fy1) of the flux column, every level
         a.flux_norm = c->cfg.flux_norm;
@@ -398,6 +449,34 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
         a.c = c->coef;
         a.k = c->kc;
         a.variant = c->variant;
+        if (merged) {
+            if (j > 0) {  // the force of level j-1, read by the previous launch
+                a.fdclr = fd[(j - 1) % 3];
+                a.flclr = fl[(j - 1) % 3];
+            }
+            if (j < K - 1) {
+                a.fkeep = 1;
+                const float *ps, *pus;
+                const int* pe;
+                pts_of(c, c->t + j, &ps, &pus, &pe);  // force^{t+j+1}: the points of iteration t+j
+                int clo, chi;
+                force_clip(c, j + 1, true, &clo, &chi);
+                a.nns = c->ns;
+                a.nG = IbGhost{c->nx, c->x_begin, D, clo, chi, 0};
+                a.n_s = ps;
+                a.n_us = pus;
+                a.n_eps = pe;
+                a.fdnext = fd[(j + 1) % 3];
+                a.flnext = fl[(j + 1) % 3];
+            } else {  // level K-2's force in the ghost columns it may reach (no own entries there)
+                int clo, chi;
+                force_clip(c, K - 2, true, &clo, &chi);
+                a.clr_w = std::max(0, std::min(-clo, chi - c->ncol));
+                a.clr_lo = -a.clr_w;
+                a.clr_hi = c->ncol;
+                a.clr_waves = 2 * a.clr_w * c->nch;
+            }
+        }
         hipStream_t ls = bs;
         if (j == K - 1) {
             if (bs != ds) {  // behind the deep sweep, on its stream
@@ -406,9 +485,9 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
                 ls = ds;
             }
             if (slab && D > 0) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_bnd, 0));
-            if (a.ncols <= 0) HIP_TRY(c, hipEventRecord(c->band_end, ls));
+            if (a.ncols <= 0 && a.clr_waves <= 0) HIP_TRY(c, hipEventRecord(c->band_end, ls));
         }
-        if (a.ncols <= 0) continue;
+        if (a.ncols <= 0 && a.nns <= 0 && a.clr_waves <= 0) continue;
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, ls))) return rc;
         HIP_TRY(c, launch_fused<T>(a, ls, j == K - 1 ? c->band_end : nullptr));
@@ -531,6 +610,12 @@ int band_release(iblb_ctx* c) {
     }
     if (c->s_alloc) (void)hipFree(c->s_alloc);
     c->s_alloc = nullptr;
+    if (c->bf_alloc) (void)hipFree(c->bf_alloc);
+    if (c->bfl_alloc) (void)hipFree(c->bfl_alloc);
+    c->bf_alloc = nullptr;
+    c->bfl_alloc = nullptr;
+    c->bfd[0] = c->bfd[1] = nullptr;
+    c->bfl[0] = c->bfl[1] = nullptr;
     return IBLB_OK;
 }
 

@@ -8,7 +8,7 @@
 // the collide-stream kernels read).
 #pragma once
 
-#include "iblb_kernels.h"
+#include "lbm_vec.h"
 
 namespace iblb {
 
@@ -171,6 +171,128 @@ __device__ __forceinline__ void ib_ghost_group(const T* __restrict__ g, const La
         if (n < 9)
             spread_node(L, G.nx, G.x_begin - m * G.nx, x, y, xs, ys, Fx, Fy, e, fd, fplane, flags, nch, rows_per_chunk,
                         G.clo, G.chi);
+    }
+}
+
+// ---- merged band chain: the next level's force from inside a level's launch ----------------
+// A band level's launch computes g^{t+j+1} from g^{t+j}; the force of level j+1 needs g^{t+j+1} at
+// the nodes of the points of iteration t+j, which other waves of the same launch are writing.  So
+// the point's 16-lane group recomputes this level's collide over the cells its nodes pull: node
+// columns xl0-1 .. xl0+1 pull columns xl0-2 .. xl0+2, node rows y0-1 .. y0+1 (y0-2 .. y0+2 with the
+// flat-index quirk) pull rows y0-3 .. y0+3 — a 5 x 7 region — with the pull, force and storage
+// rounding of fused_wave (bit for bit the values the level writes), into LDS; then nodes -> F_s ->
+// spread into the next level's force buffer, as ib_ghost_group.
+constexpr int NEXT_RW = 5, NEXT_RH = 7, NEXT_CELLS = NEXT_RW * NEXT_RH;
+
+// this level's post-collision values of cell (xc, y), all nine planes, as fused_wave stores them:
+// the loads (pulls, chunk flag, dense force: zero where no flag is set) ...
+template <typename T>
+struct CellIn {
+    T v[9];
+    double fx, fy;
+    bool hf;
+};
+template <typename T>
+__device__ __forceinline__ void level_cell_load(const FusedArgs<T>& a, int xc, int y, int rows_per_chunk, CellIn<T>& in) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) in.v[k] = pull_direct<T>(a.src, a.L, xc, y, k);
+    in.hf = a.flags[(long)xc * a.nch + y / rows_per_chunk] != 0;
+    in.fx = a.fdense[(long)xc * a.L.rows + y];
+    in.fy = a.fdense[a.fplane + (long)xc * a.L.rows + y];
+}
+// ... and the collide
+template <typename T>
+__device__ __forceinline__ void level_cell_collide(const FusedArgs<T>& a, const CellIn<T>& in, T out[9]) {
+    typedef typename Calc<T>::R R;
+    constexpr bool DEV = Store<T>::dev;
+    R f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = (R)in.v[k];
+    const KBase<R>& kb = kbase<R>(a.k);
+    if (in.hf) relax_cell<R, DEV>(f, kb, make_kforce<R>(kb, (R)(a.c.gx + in.fx), (R)(a.c.gy + in.fy)));
+    else relax_cell<R, DEV>(f, kb, kbody<R>(a.k));
+#pragma unroll
+    for (int k = 0; k < 9; ++k) out[k] = (T)f[k];
+}
+
+// point k (pt: k < nns, uniform over the group), lane n of its group, region slot `reg` (LDS,
+// NEXT_CELLS x 9 values); every lane of the group must call it (shuffles).  The region is 5 x 5
+// cells (rows y0-2 .. y0+2) unless a node crosses the lattice's x edge (the flat-index quirk moves
+// it a row: 5 x 7, rows y0-3 .. y0+3); each lane loads all of its (two or three) cells before it
+// collides them.
+template <typename T>
+__device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, int k, int n, int rows_per_chunk,
+                                              T (*reg)[9]) {
+#pragma clang fp contract(off)
+    const IbGhost& G = a.nG;
+    const Layout& L = a.L;
+    float xs = 0.f, ys = 0.f;
+    int x0 = 0, y0 = 0;
+    if (pt) {
+        xs = a.n_s[2 * k + 0];
+        ys = a.n_s[2 * k + 1];
+        x0 = node_x0(xs);
+        y0 = node_x0(ys);
+    }
+    const int e = pt ? (a.n_eps ? a.n_eps[k] : 1) : 0;
+    const bool quirk = x0 - 1 < 0 || x0 + 1 >= G.nx;  // group-uniform
+    const int ry0 = quirk ? y0 - 3 : y0 - 2, ncell = NEXT_RW * (quirk ? NEXT_RH : NEXT_RH - 2);
+    for (int m = -1; m <= 1; ++m) {
+        const int xl0 = x0 - G.x_begin + m * G.nx;
+        // group-uniform: does this image spread into [clo, chi)?
+        const bool img = pt && xl0 + 1 >= G.clo && xl0 - 1 < G.chi;
+        if (!img) continue;
+        // the region: this level's values of columns xl0-2 .. xl0+2 (cells whose own pulls stay inside
+        // the buffer and rows inside the lattice; the others are never read below)
+        // cells n and n+16 loaded together, then collided; n+32 (5 x 7 regions only) after them
+        for (int r = 0; r < ncell; r += 2 * LANES_PER_POINT) {
+            CellIn<T> in[2];
+            bool ok[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int c = r + n + LANES_PER_POINT * i;
+                const int xc = xl0 - 2 + c % NEXT_RW, y = ry0 + c / NEXT_RW;
+                ok[i] = c < ncell && y >= 0 && y < L.ny && xc - 1 >= -G.gc && xc + 1 < L.ncol + G.gc;
+                if (ok[i]) level_cell_load<T>(a, xc, y, rows_per_chunk, in[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                if (ok[i]) level_cell_collide<T>(a, in[i], reg[r + n + LANES_PER_POINT * i]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double tx = 0., ty = 0.;
+        bool valid = false;
+        const int xn = xl0 + cx(n), x = x0 + cx(n), y = y0 + cy(n);
+        if (n < 9) {
+            const long j = (long)y * G.nx + x;  // flat index without wrap (ImmersedBoundary.cu:119-122)
+            // the node's pulls read region columns xn-1 .. xn+1, whose own pulls reach xn-2 .. xn+2
+            if (j >= 0 && j < (long)G.nx * L.ny && xn - 2 >= -G.gc && xn + 2 < L.ncol + G.gc) {
+                const int yj = (int)(j / G.nx);
+                const int rx = xn - (xl0 - 2), ry = yj - ry0;
+                double f[9];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) {  // pull_direct on g^{t+j+1}, from the region
+                    T v;
+                    if (yj == 0 && cy(q) == 1) v = reg[ry * NEXT_RW + rx][q == 2 ? 4 : (q == 5 ? 7 : 8)];
+                    else if (yj == L.ny - 1 && cy(q) == -1) v = reg[ry * NEXT_RW + rx][q == 4 ? 2 : (q == 8 ? 5 : 6)];
+                    else v = reg[(ry - cy(q)) * NEXT_RW + rx - cx(q)][q];
+                    f[q] = Store<T>::to_f(v, q);
+                }
+                node_term(f, xs, ys, x, y, a.n_us[2 * k + 0], a.n_us[2 * k + 1], tx, ty);
+                valid = true;
+            }
+        }
+        float Fx, Fy;
+        fold_terms(tx, ty, valid, Fx, Fy);
+        if (n < 9)
+            spread_node(L, G.nx, G.x_begin - m * G.nx, x, y, xs, ys, Fx, Fy, e, a.fdnext, a.fplane, a.flnext, a.nch,
+                        rows_per_chunk, G.clo, G.chi);
+        // the region slot is rewritten by the next image: every lane's reads above come first
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 

@@ -342,6 +342,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 1 : 3);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
+    c->band_merge = (int)env_long("IBLB_BAND_MERGE", 1);
     // one cell per lane in a group slab's deep sweeps (self ring 512 / 1024 / 2048 x 4096: 0.0347 /
     // 0.0542 / 0.0935 ms/iteration vs 0.0380 / 0.0568 / 0.0942 with two, profiles/r01e7_*)
     c->slab_vs = 1;

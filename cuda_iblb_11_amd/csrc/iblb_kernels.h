@@ -12,6 +12,14 @@ namespace iblb {
 template <typename T>
 constexpr int vec_of() { return 16 / (int)sizeof(T); }
 
+// A slab's view of the points for IB with ghost columns (launch_ib_ghost below)
+struct IbGhost {
+    int nx, x_begin;
+    int gc;        // ghost columns holding valid data (node pulls outside are skipped)
+    int clo, chi;  // local columns that receive force
+    int part;
+};
+
 template <typename T>
 struct FusedArgs {
     const T* src;
@@ -43,6 +51,24 @@ struct FusedArgs {
     int row_tab = 0;
     int nchl = 0;
     int store_rows = 0;
+    // Merged band chain (ctx_band.hip): the force of this level is read, not consumed (fkeep: the
+    // IB waves below read it too); the waves of the entries clear the force buffer fdclr / flclr
+    // of the level before (consumed by the previous launch) at their (column, chunk); clr_waves
+    // more waves clear it at columns clr_lo .. clr_lo+clr_w-1 and clr_hi .. clr_hi+clr_w-1 (nch
+    // chunks each); nns > 0: after those,
+    // 16 lanes per point (nns points of the next level's iteration) evaluate the next level's force
+    // from this launch's source (ib_next_group, ib_device.h) into fdnext / flnext.
+    int fkeep = 0;
+    double* fdclr = nullptr;
+    uint8_t* flclr = nullptr;
+    int clr_waves = 0, clr_lo = 0, clr_hi = 0, clr_w = 0;
+    int nns = 0;
+    IbGhost nG{};
+    const float* n_s = nullptr;
+    const float* n_us = nullptr;
+    const int* n_eps = nullptr;
+    double* fdnext = nullptr;
+    uint8_t* flnext = nullptr;
 };
 
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.
@@ -135,12 +161,7 @@ hipError_t launch_ib_point(const T* g, Layout L, Halo<T> H, int nx, int ns, cons
 // column min(x0, XDIM-1) writes the point's F_s, the others zero (readers sum).  part: 0 every
 // point, 1 the inner points (2 <= x0 - x_begin <= ncol-3: nodes and pulls inside the slab, no
 // ghost needed), 2 the others.
-struct IbGhost {
-    int nx, x_begin;
-    int gc;        // ghost columns holding valid data (node pulls outside are skipped)
-    int clo, chi;  // local columns that receive force
-    int part;
-};
+// (IbGhost: declared with FusedArgs above)
 template <typename T>
 hipError_t launch_ib_ghost(const T* g, Layout L, IbGhost G, int ns, const float* s, const float* u_s, const int* eps,
                            float* F_s, double* fdense, long fplane, uint8_t* flags, int nch, int rows_per_chunk,

@@ -13,6 +13,19 @@
 
 namespace iblb {
 
+// merged band chain: clear the force buffer the previous launch consumed at (column xc, chunk ch)
+template <int V>
+__device__ __forceinline__ void band_clear(double* fd, uint8_t* fl, long fplane, int rows, int nch, int xc, int ch,
+                                           int y0, int lane) {
+    const long fi = (long)xc * nch + ch;
+    if (fl[fi]) {
+        double* p = fd + (long)xc * rows + y0;
+#pragma unroll
+        for (int e = 0; e < V; ++e) { p[e] = 0.; p[fplane + e] = 0.; }
+        if (lane == 0) fl[fi] = 0;
+    }
+}
+
 // One wave = one (column, chunk of 64*V rows); lane l owns rows y0 .. y0+V-1.
 // Column-uniform decisions (halo source, flux column, IB flag) are scalar branches.  Walls are
 // per-lane fixes of the first / last row.  Columns outside [0, ncol) (IB band trapezoids over a
@@ -93,9 +106,14 @@ __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, 
         double* fx = a.fdense + (long)xc * L.rows + y0;
         double* fy = a.fdense + a.fplane + (long)xc * L.rows + y0;
 #pragma unroll
-        for (int e = 0; e < V; ++e) { fxv[e] = fx[e]; fyv[e] = fy[e]; fx[e] = 0.; fy[e] = 0.; }
-        if (lane == 0) a.flags[(long)xc * a.nch + ch] = 0;  // only this wave reads this flag
+        for (int e = 0; e < V; ++e) { fxv[e] = fx[e]; fyv[e] = fy[e]; }
+        if (!a.fkeep) {
+#pragma unroll
+            for (int e = 0; e < V; ++e) { fx[e] = 0.; fy[e] = 0.; }
+            if (lane == 0) a.flags[(long)xc * a.nch + ch] = 0;  // only this wave reads this flag
+        }
     }
+    if (IB && a.flclr) band_clear<V>(a.fdclr, a.flclr, a.fplane, L.rows, a.nch, xc, ch, y0, lane);
 
     const bool do_flux = a.flux_col >= 0 && xc == a.flux_col;  // (-1: none; ghost column -1 is a real column)
     double q = 0.;
@@ -142,9 +160,46 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
                                threadIdx.x & 63);
 }
 
+// A level of the merged band chain (FusedArgs: fkeep, fdclr, clr_waves, nns): the waves of the
+// table entries (fused_wave), then clr_waves clear-only waves, then the 16-lane point groups of the
+// next level's IB (ib_next_group).  The roles are wave-uniform; the point groups synchronise only
+// within their wave (LDS region per group).
+template <typename T, int V, int MODE>
+__global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
+    __shared__ T reg[256 / LANES_PER_POINT][NEXT_CELLS][9];
+    const int lane = threadIdx.x & 63;
+    const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int ew = a.ncols * a.nchl;
+    if (gw < ew) {
+        fused_wave<T, V, true, MODE>(a, gw, lane);
+        return;
+    }
+    if (gw < ew + a.clr_waves) {
+        const int c = gw - ew, per = a.clr_w * a.nch;
+        const int r = c < per ? c : c - per;
+        const int xc = (c < per ? a.clr_lo : a.clr_hi) + r / a.nch, ch = r % a.nch;
+        band_clear<V>(a.fdclr, a.flclr, a.fplane, a.L.rows, a.nch, xc, ch, ch * 64 * V + lane * V, lane);
+        return;
+    }
+    const long t = (long)(gw - ew - a.clr_waves) * 64 + lane;
+    const int k = (int)(t / LANES_PER_POINT), n = (int)(t % LANES_PER_POINT);
+    ib_next_group<T>(a, k < a.nns, k, n, 64 * V, reg[threadIdx.x / LANES_PER_POINT]);
+}
+
+template <typename T, int MODE>
+hipError_t launch_band_level_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t s, hipEvent_t stop) {
+    constexpr int V = vec_of<T>();
+    if (stop)
+        hipExtLaunchKernelGGL(band_level_kernel<T, V, MODE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, a);
+    else
+        band_level_kernel<T, V, MODE><<<blocks, 256, 0, s>>>(a);
+    return hipGetLastError();
+}
+
 template <typename T, int MODE>
 hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t s, hipEvent_t stop) {
     constexpr int V = vec_of<T>();
+    if (a.row_tab && (a.nns > 0 || a.clr_waves > 0)) return launch_band_level_mode<T, MODE>(a, blocks, s, stop);
     if (stop) {  // the event rides on the kernel's own completion signal: no marker packet after it
         if (a.flags)
             hipExtLaunchKernelGGL(fused_kernel<T, V, true, MODE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, a);
@@ -160,8 +215,10 @@ hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t
 
 template <typename T>
 hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s, hipEvent_t stop) {
-    const long waves = (long)a.ncols * (a.row_tab ? a.nchl : a.nch);
+    long waves = (long)a.ncols * (a.row_tab ? a.nchl : a.nch);
+    if (a.row_tab) waves += a.clr_waves + ((long)a.nns * LANES_PER_POINT + 63) / 64;
     if (waves <= 0) return hipSuccess;
+    if (a.row_tab && (a.nns > 0 || a.clr_waves > 0) && !a.flags) return hipErrorInvalidValue;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     switch (a.variant) {
         case 1: return launch_fused_mode<T, 1>(a, blocks, s, stop);

@@ -708,6 +708,36 @@ def test_ib_band_near_lattice_edges(gpu, oracle, precision, monkeypatch):
     assert abs(lat.flux - sim.flux) <= (1e-9 if precision == "f64" else 1e-4) * max(abs(sim.flux), 1e-30)
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_ib_band_merged_equals_chained(gpu, oracle, precision, monkeypatch):
+    """The merged band chain (IBLB_BAND_MERGE=2; the default 1 picks it for short deep sweeps: each
+    level's launch also evaluates the next level's force, its point groups recomputing the level's
+    collide over their nodes' pulls) against the chained one (=0: an IB launch before every level), on filaments across x = 0, next to
+    x = XDIM-1 and mid-lattice, chunked calls with readers between them: equal up to the arrival
+    order of the spread atomics, and both against the oracle."""
+    nx, ny = 160, 96
+    a, b, c = _line(0.4, 30), _line(nx - 1.3, 24, y0=40.0), _line(70.3, 40, y0=20.0)
+    a[0][0::2] = np.mod(a[0][0::2], nx)
+    pts = tuple(np.concatenate([p, q, r]) for p, q, r in zip(a, b, c))
+    runs = {}
+    for merge in ("2", "0"):  # always / never (the default, 1, merges where the deep sweep is short)
+        monkeypatch.setenv("IBLB_BAND_MERGE", merge)
+        lat, sim = _static_run(gpu, oracle, nx, ny, 33, pts, chunks=(1, 12, 5, 15), precision=precision,
+                               monkeypatch=monkeypatch)
+        tm = lat.timing()
+        assert tm["sweepk_launches"] >= 5, tm
+        runs[merge] = (lat.macro(), lat.force(), lat.flux, tm)
+        check_fields(lat, sim, 1e-9 if precision == "f64" else TOL32)
+        lat.close()
+    monkeypatch.delenv("IBLB_BAND_MERGE")
+    # merged: one IB launch per cycle at most (the force owed at its start), chained: K of them
+    assert runs["2"][3]["ib_ms"] < 0.6 * runs["0"][3]["ib_ms"], (runs["2"][3], runs["0"][3])
+    (r1, u1), (r0, u0) = runs["2"][0], runs["0"][0]
+    tol = (1e-13, 1e-11) if precision == "f64" else (1e-6, 1e-5)
+    assert rel(r1, r0) <= tol[0] and rel(u1, u0) <= tol[1]
+    assert abs(runs["2"][2] - runs["0"][2]) <= (1e-11 if precision == "f64" else 1e-5) * max(abs(runs["0"][2]), 1e-30)
+
+
 def _ulps(a, b):
     """Distance of two float32 arrays in units in the last place."""
     ia = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
