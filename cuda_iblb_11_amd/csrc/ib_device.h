@@ -35,16 +35,17 @@ __device__ __forceinline__ void spread_node(const Layout& L, int nx, int x_begin
     flags[(long)xc * nch + y / rows_per_chunk] = 1;
 }
 
-// F_s of the group's point from the per-lane node terms, in node order 0..8
+// F_s of the group's point from the per-lane node terms, in node order 0..8 (groups of W lanes)
+template <int W = LANES_PER_POINT>
 __device__ __forceinline__ void fold_terms(double tx, double ty, bool valid, float& Fx, float& Fy) {
 #pragma clang fp contract(off)
     Fx = 0.f;
     Fy = 0.f;
 #pragma unroll
     for (int m = 0; m < 9; ++m) {
-        const double ax = __shfl(tx, m, LANES_PER_POINT);
-        const double ay = __shfl(ty, m, LANES_PER_POINT);
-        if (__shfl((int)valid, m, LANES_PER_POINT)) {
+        const double ax = __shfl(tx, m, W);
+        const double ay = __shfl(ty, m, W);
+        if (__shfl((int)valid, m, W)) {
             Fx = (float)((double)Fx + ax);
             Fy = (float)((double)Fy + ay);
         }
@@ -183,6 +184,7 @@ __device__ __forceinline__ void ib_ghost_group(const T* __restrict__ g, const La
 // rounding of fused_wave (bit for bit the values the level writes), into LDS; then nodes -> F_s ->
 // spread into the next level's force buffer, as ib_ghost_group.
 constexpr int NEXT_RW = 5, NEXT_RH = 7, NEXT_CELLS = NEXT_RW * NEXT_RH;
+constexpr int NEXT_LANES = 32;  // lanes per point: one region cell per lane (5 x 5), a second for 3 lanes (5 x 7)
 
 // this level's post-collision values of cell (xc, y), all nine planes, as fused_wave stores them:
 // the loads (pulls, chunk flag, dense force: zero where no flag is set) ...
@@ -215,11 +217,10 @@ __device__ __forceinline__ void level_cell_collide(const FusedArgs<T>& a, const 
     for (int k = 0; k < 9; ++k) out[k] = (T)f[k];
 }
 
-// point k (pt: k < nns, uniform over the group), lane n of its group, region slot `reg` (LDS,
-// NEXT_CELLS x 9 values); every lane of the group must call it (shuffles).  The region is 5 x 5
-// cells (rows y0-2 .. y0+2) unless a node crosses the lattice's x edge (the flat-index quirk moves
-// it a row: 5 x 7, rows y0-3 .. y0+3); each lane loads all of its (two or three) cells before it
-// collides them.
+// point k (pt: k < nns, uniform over the group of NEXT_LANES lanes), lane n of its group, region
+// slot `reg` (LDS, NEXT_CELLS x 9 values); every lane of the group must call it (shuffles).  The
+// region is 5 x 5 cells (rows y0-2 .. y0+2), one per lane, unless a node crosses the lattice's x
+// edge (the flat-index quirk moves it a row: 5 x 7, rows y0-3 .. y0+3).
 template <typename T>
 __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, int k, int n, int rows_per_chunk,
                                               T (*reg)[9]) {
@@ -244,20 +245,14 @@ __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, in
         if (!img) continue;
         // the region: this level's values of columns xl0-2 .. xl0+2 (cells whose own pulls stay inside
         // the buffer and rows inside the lattice; the others are never read below)
-        // cells n and n+16 loaded together, then collided; n+32 (5 x 7 regions only) after them
-        for (int r = 0; r < ncell; r += 2 * LANES_PER_POINT) {
-            CellIn<T> in[2];
-            bool ok[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int c = r + n + LANES_PER_POINT * i;
-                const int xc = xl0 - 2 + c % NEXT_RW, y = ry0 + c / NEXT_RW;
-                ok[i] = c < ncell && y >= 0 && y < L.ny && xc - 1 >= -G.gc && xc + 1 < L.ncol + G.gc;
-                if (ok[i]) level_cell_load<T>(a, xc, y, rows_per_chunk, in[i]);
+        // cell n (and n+32: the three extra cells of a 5 x 7 region)
+        for (int c = n; c < ncell; c += NEXT_LANES) {
+            const int xc = xl0 - 2 + c % NEXT_RW, y = ry0 + c / NEXT_RW;
+            if (y >= 0 && y < L.ny && xc - 1 >= -G.gc && xc + 1 < L.ncol + G.gc) {
+                CellIn<T> in;
+                level_cell_load<T>(a, xc, y, rows_per_chunk, in);
+                level_cell_collide<T>(a, in, reg[c]);
             }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-                if (ok[i]) level_cell_collide<T>(a, in[i], reg[r + n + LANES_PER_POINT * i]);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -285,7 +280,7 @@ __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, in
             }
         }
         float Fx, Fy;
-        fold_terms(tx, ty, valid, Fx, Fy);
+        fold_terms<NEXT_LANES>(tx, ty, valid, Fx, Fy);
         if (n < 9)
             spread_node(L, G.nx, G.x_begin - m * G.nx, x, y, xs, ys, Fx, Fy, e, a.fdnext, a.fplane, a.flnext, a.nch,
                         rows_per_chunk, G.clo, G.chi);

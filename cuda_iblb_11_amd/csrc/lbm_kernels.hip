@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
 // within their wave (LDS region per group).
 template <typename T, int V, int MODE>
 __global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
-    __shared__ T reg[256 / LANES_PER_POINT][NEXT_CELLS][9];
+    __shared__ T reg[256 / NEXT_LANES][NEXT_CELLS][9];
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int ew = a.ncols * a.nchl;
@@ -182,8 +182,8 @@ __global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
         return;
     }
     const long t = (long)(gw - ew - a.clr_waves) * 64 + lane;
-    const int k = (int)(t / LANES_PER_POINT), n = (int)(t % LANES_PER_POINT);
-    ib_next_group<T>(a, k < a.nns, k, n, 64 * V, reg[threadIdx.x / LANES_PER_POINT]);
+    const int k = (int)(t / NEXT_LANES), n = (int)(t % NEXT_LANES);
+    ib_next_group<T>(a, k < a.nns, k, n, 64 * V, reg[threadIdx.x / NEXT_LANES]);
 }
 
 template <typename T, int MODE>
@@ -216,7 +216,7 @@ hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t
 template <typename T>
 hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s, hipEvent_t stop) {
     long waves = (long)a.ncols * (a.row_tab ? a.nchl : a.nch);
-    if (a.row_tab) waves += a.clr_waves + ((long)a.nns * LANES_PER_POINT + 63) / 64;
+    if (a.row_tab) waves += a.clr_waves + ((long)a.nns * NEXT_LANES + 63) / 64;
     if (waves <= 0) return hipSuccess;
     if (a.row_tab && (a.nns > 0 || a.clr_waves > 0) && !a.flags) return hipErrorInvalidValue;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
