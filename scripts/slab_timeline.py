@@ -2,12 +2,12 @@
 
 Prints per kernel kind (interior sweep, boundary sweep, pack, RCCL, other) the mean duration over
 the last 100 cycles and the mean gap between consecutive interior sweeps (the cycle time)."""
-import csv, glob, statistics, sys
+import csv, glob, re, statistics, sys
 
 
 def kind(name):
-    if "sweepk_kernel" in name:
-        return "sweep_slab" if ", true>" in name or ",true>" in name else "sweep"
+    if "sweepk_kernel" in name:  # sweepk_kernel<T, VS, MODE, K, SLAB[, WPE]>: SLAB = the boundary sweeps
+        return "sweep_slab" if re.search(r",\s*true\s*(,\s*\d+\s*)?>", name) else "sweep"
     if "pack" in name:
         return "pack"
     if "nccl" in name.lower():
@@ -35,7 +35,8 @@ def main(d):
         print(f"  {k:30s} n={len(v):5d} mean {statistics.mean(v):8.2f} us  per cycle {sum(v) / len(ints):8.2f} us")
     # critical path hints: idle gap on the compute stream between interior sweeps
     gaps = [(b[0] - a[1]) / 1e3 for a, b in zip(ints, ints[1:])]
-    print(f"  gap between interior sweeps: mean {statistics.mean(gaps):.2f} us, max {max(gaps):.2f} us")
+    print(f"  gap between interior sweeps: mean {statistics.mean(gaps):.2f} us, median {statistics.median(gaps):.2f} us, "
+          f"max {max(gaps):.2f} us")
 
 
 
