@@ -1,4 +1,5 @@
 #!/bin/bash
+# (IBLB_BND_VS and the two-wave f64 variant were temporary experiment hooks, removed after these runs: profiles/r03bv, r03w2)
 # Group-slab boundary sweeps with two cells per lane (IBLB_BND_VS=2: 35 row chunks, one wave per
 # SIMD -> 24 reserved CUs at 4096 rows instead of 32) vs one (default): slab tests, then the
 # strong-scaling self rings 512 / 1024 / 2048 x 4096, alternated twice.
