@@ -85,8 +85,9 @@ struct Sweep2Args {
     int vs;              // cells per lane; rows, col and plane multiples of vs
     int nch;             // set by launch_sweep2
     int variant;         // deep sweeps: bit 0 nontemporal stores, bit 1 the f32 wall split
-    int nsweep_w = 0;    // wall split (set by the launcher): sweeps of the wall-row chunks,
-    int wall_ch0 = 0;    // and the first wall-row chunk after chunk 0
+    int nsweep_w = 0;    // wall split (set by the launcher): sweeps of each wall chunk,
+    int wall_ch0 = 0;    // inner chunks between the wall chunks,
+    int wall_top = 0;    // and the first row of the top wall chunk
     int cus;             // deep sweeps, balanced widths: CUs the launch's stream may use (0 = all)
     int flux_col;        // local column sampled for Q (every iteration), or -1
     int fskip0, fskip1;  // rows [fskip0, fskip1) of the flux column are not sampled (an IB band

@@ -35,7 +35,9 @@
 
 namespace iblb {
 
-enum { MODE_NO_PREFETCH = 8 };  // sweep only (MODE bits 1, 2 as in lbm_vec.h)
+// sweep only (MODE bits 1, 2 as in lbm_vec.h): no software prefetch of the next column (two-step
+// sweeps); the deep sweep's wall split (sweepk_kernel)
+enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16 };
 
 namespace {
 
@@ -642,13 +644,15 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
 template <int K, int VS>
 constexpr int ghost_lanes() { return (K - 1 + VS - 1) / VS; }
 
-// Wall split (WPE > 1, balanced sweeps only): the wall-row chunks — chunk 0 and the chunks from
-// a.wall_ch0 on — are walked by their own family of a.nsweep_w sweeps, listed after the
-// a.nsweep sweeps of the inner chunks [1, a.wall_ch0).  The kernel is built for WPE waves per SIMD
-// (f32: 3 instead of 2; the wall walk then spills a few VGPRs and is slower per column), and the
-// wall family's narrower sweeps let those waves finish with the others in the launch's one round.
-__device__ __forceinline__ void split_item(const int nin, const int nsw_in, const int nwall, int wv, int& sw, int& ch,
-                                           bool& wall) {
+// Wall split (MODE_SPLIT, balanced sweeps only).  The rows split into a bottom wall chunk [0, OWN1),
+// the inner rows [OWN1, a.wall_top) in chunks of OWN*VS and a top wall chunk [a.wall_top, ny), where
+// OWN1 = 64 - 2(K-1) rows is one wave of one cell per lane.  The inner chunks are walked by the
+// kernel's VS-cell walk without wall code (a.nsweep sweeps each); the two wall chunks by a one-cell
+// walk with the wall rules (a.nsweep_w sweeps each), listed after them.  The kernel is built for
+// WPE waves per SIMD (f32: 3 instead of 2): the one-cell wall walk needs fewer registers than the
+// inner walk, so neither spills (the VS-cell wall walk spilled 15 dwords and ran ~1.4x slower per
+// column, profiles/r03sp).
+__device__ __forceinline__ void split_item(const int nin, const int nsw_in, int wv, int& sw, int& ch, bool& wall) {
     int b = (int)blockIdx.x;
     const int q = (int)gridDim.x / 8;
     if (b < 8 * q) b = (b % 8) * q + b / 8;
@@ -657,12 +661,11 @@ __device__ __forceinline__ void split_item(const int nin, const int nsw_in, cons
     wall = gw >= ni;
     if (!wall) {
         sw = gw / nin;
-        ch = 1 + (gw - sw * nin);
+        ch = gw - sw * nin;
     } else {
         const int g2 = gw - ni;
-        sw = g2 / nwall;
-        const int wc = g2 - sw * nwall;
-        ch = wc == 0 ? 0 : nin + wc;
+        sw = g2 >> 1;
+        ch = g2 & 1;  // 0: bottom, 1: top
     }
 }
 
@@ -674,15 +677,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int sw, ch, nsw = a.nsweep;
-    if (WPE > 1) {
-        bool wall;
-        const int nin = a.wall_ch0 - 1;
-        split_item(nin, a.nsweep, a.nch - nin, wv, sw, ch, wall);
+    bool wall = false;
+    if (MODE & MODE_SPLIT) {
+        split_item(a.wall_ch0, a.nsweep, wv, sw, ch, wall);
         if (wall) nsw = a.nsweep_w;
+        if (sw >= nsw) return;
     } else {
         linear_item(a.nch, wv, sw, ch);
+        if (sw >= nsw || ch >= a.nch) return;
     }
-    if (sw >= nsw || ch >= a.nch) return;
     int xa, xb;
     if (a.col_step > 0) {
         xa = a.col_begin + sw * a.col_step;
@@ -692,22 +695,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         xa = a.col_begin + (int)(sw * n / nsw);
         xb = a.col_begin + (int)((sw + 1) * n / nsw);
     }
-    const int cs = ch * (OWN * VS);
-    const int row0 = cs - G * VS;
-    const int r0 = row0 + lane * VS;
-    const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
-    const int et = a.L.ny - 1 - r0;
-    const bool owner = lane >= G && lane < 64 - G && r0 < a.L.ny;
-    const bool bot = r0 == 0;
-    const bool top = et >= 0 && et < VS;
-    // wave-uniform: does the wave hold a wall row (y = 0 or Y-1, ghost lanes included)?
-    const bool walls = row0 <= 0 || row0 + 64 * VS >= a.L.ny;
     const bool rev = sw & 1;
-    const double q =
-        walls ? (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
-                     : sweepk_walk<T, VS, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top))
-              : (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
-                     : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top));
+    double q;
+    if ((MODE & MODE_SPLIT) && wall) {  // a wall chunk: one cell per lane, the wall walk
+        constexpr int G1 = ghost_lanes<K, 1>(), OWN1 = 64 - 2 * G1;
+        const int cs = ch == 0 ? 0 : a.wall_top;
+        const int row0 = cs - G1;
+        const int r0 = row0 + lane;
+        const unsigned off = (unsigned)(lane * (int)sizeof(T));
+        const int et = a.L.ny - 1 - r0;
+        const bool owner = lane >= G1 && lane < 64 - G1 && r0 < a.L.ny && (ch == 1 || r0 < OWN1);
+        q = rev ? sweepk_walk<T, 1, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0)
+                : sweepk_walk<T, 1, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0);
+    } else if (MODE & MODE_SPLIT) {  // an inner chunk: no wall row within reach of its own rows
+        constexpr int OWN1 = 64 - 2 * ghost_lanes<K, 1>();
+        const int cs = OWN1 + ch * (OWN * VS);
+        const int row0 = cs - G * VS;
+        const int r0 = row0 + lane * VS;
+        const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
+        const int et = a.L.ny - 1 - r0;
+        const bool owner = lane >= G && lane < 64 - G && r0 < a.wall_top;
+        q = rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false)
+                : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false);
+    } else {
+        const int cs = ch * (OWN * VS);
+        const int row0 = cs - G * VS;
+        const int r0 = row0 + lane * VS;
+        const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
+        const int et = a.L.ny - 1 - r0;
+        const bool owner = lane >= G && lane < 64 - G && r0 < a.L.ny;
+        const bool bot = r0 == 0;
+        const bool top = et >= 0 && et < VS;
+        // wave-uniform: does the wave hold a wall row (y = 0 or Y-1, ghost lanes included)?
+        const bool walls = row0 <= 0 || row0 + 64 * VS >= a.L.ny;
+        q = walls ? (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
+                         : sweepk_walk<T, VS, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top))
+                  : (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
+                         : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top));
+    }
     if (a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb) {
         const double qs = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, qs);
@@ -736,10 +761,11 @@ static long resident_waves(int cus) {
     return waves_per_cu<T, VS, MODE, K, SLAB, WPE>() * (cus > 0 ? std::min(cus, ncu) : ncu);
 }
 
-// wall split: sweeps of a wall-row chunk per sweep of an inner chunk, in quarters (the wall walk
-// of the 3-wave f32 build spills and runs ~1.4x slower per column; M f32 per launch with 1, 1.5, 2,
-// 2.25, 2.5, 3: 0.455, 0.370, 0.305-0.320, 0.329, 0.314, 0.326 ms, profiles/r03sp, r03r2)
-constexpr int WALL_SWEEPS_X4 = 8;
+// wall split: sweeps of a wall chunk per sweep of an inner chunk, in quarters.  With one-cell wall
+// walks (no spills) the launch time is the inner waves' whatever the ratio: M f32 0.319-0.322 ms per
+// launch for 0.5 ... 1.5 (profiles/r03s1); the first split (two-cell wall walks with spills) needed 2
+// (0.305-0.320 ms, profiles/r03sp, r03r2).
+constexpr int WALL_SWEEPS_X4 = 4;
 
 template <typename T, int VS, int MODE, int K, bool SLAB, int WPE>
 static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t stop, hipEvent_t start) {
@@ -751,16 +777,16 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
         const long n = b.col_end - b.col_begin;
         const long slots = resident_waves<T, VS, MODE, K, SLAB, WPE>(b.cus);
         long ns = (n + b.W - 1) / b.W;
-        if (WPE > 1) {
-            // wall split: nin inner chunks with ns sweeps, nwall wall chunks with ns * r sweeps
-            const long nin = b.wall_ch0 - 1, nwall = b.nch - nin, r4 = WALL_SWEEPS_X4;
+        if (MODE & MODE_SPLIT) {
+            // wall split: nin inner chunks with ns sweeps, the two wall chunks with ns * r sweeps each
+            const long nin = b.wall_ch0, r4 = WALL_SWEEPS_X4;
             if (slots > 0) {
-                const long rounds = std::max(1L, (ns * (4 * nin + r4 * nwall) / 4 + slots / 2) / slots);
-                ns = std::max(1L, 4 * rounds * slots / (4 * nin + r4 * nwall));
+                const long rounds = std::max(1L, (ns * (4 * nin + 2 * r4) / 4 + slots / 2) / slots);
+                ns = std::max(1L, 4 * rounds * slots / (4 * nin + 2 * r4));
             }
             b.nsweep = (int)std::min(ns, n);
             b.nsweep_w = (int)std::min((ns * r4 + 3) / 4, n);
-            waves = (long)b.nsweep * nin + (long)b.nsweep_w * nwall;
+            waves = (long)b.nsweep * nin + 2L * b.nsweep_w;
         } else {
             if (slots > 0) {
                 const long rounds = std::max(1L, (ns * b.nch + slots / 2) / slots);
@@ -770,7 +796,7 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
             waves = (long)b.nsweep * b.nch;
         }
     } else {
-        if (WPE > 1) return hipErrorInvalidValue;  // the split needs balanced sweeps
+        if (MODE & MODE_SPLIT) return hipErrorInvalidValue;  // the split needs balanced sweeps
         waves = (long)b.nsweep * b.nch;
     }
     const unsigned blocks = (unsigned)((waves + 3) / 4);
@@ -779,16 +805,6 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
     else
         sweepk_kernel<T, VS, MODE, K, SLAB, WPE><<<blocks, 256, 0, s>>>(b);
     return hipGetLastError();
-}
-
-// the first chunk after chunk 0 whose wave holds a wall row (ghost lanes included), as the kernel
-// decides it (row0 <= 0 || row0 + 64 VS >= ny)
-template <int K, int VS>
-inline int first_wall_chunk(int ny, int nch) {
-    constexpr int G = ghost_lanes<K, VS>();
-    for (int ch = 1; ch < nch; ++ch)
-        if (ch * (64 - 2 * G) * VS - G * VS + 64 * VS >= ny) return ch;
-    return nch;
 }
 
 // the f32 wall split (variant bit 1): two cells per lane, three waves per SIMD
@@ -802,12 +818,15 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
     Sweep2Args<T> b = a;
     b.nch = (a.L.ny + rows_per_wave - 1) / rows_per_wave;
     if constexpr (wall_split_built<T, VS>()) {
-        if ((a.variant & 2) && a.col_step <= 0) {
-            b.wall_ch0 = first_wall_chunk<K, VS>(a.L.ny, b.nch);
-            if (b.wall_ch0 >= 2) {
-                if (a.variant & 1) return launch_sweepk_mode<T, VS, 1, K, SLAB, 3>(b, s, stop, start);
-                return launch_sweepk_mode<T, VS, 0, K, SLAB, 3>(b, s, stop, start);
-            }
+        // rows: [0, OWN1) bottom wall chunk, inner chunks of rows_per_wave, top wall chunk from an even
+        // row (two-cell lanes of the inner chunks never straddle it) holding the last OWN1 or fewer rows
+        constexpr int OWN1 = 64 - 2 * ghost_lanes<K, 1>();
+        const int top = (a.L.ny - OWN1 + 1) & ~1;
+        if ((a.variant & 2) && a.col_step <= 0 && top > OWN1) {
+            b.wall_top = top;
+            b.wall_ch0 = (top - OWN1 + rows_per_wave - 1) / rows_per_wave;
+            if (a.variant & 1) return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT, K, SLAB, 3>(b, s, stop, start);
+            return launch_sweepk_mode<T, VS, MODE_SPLIT, K, SLAB, 3>(b, s, stop, start);
         }
     }
     // variants: bit 0 = nontemporal stores (default), 0 = plain
