@@ -5,7 +5,8 @@ import csv, glob, statistics, sys
 
 def short(n):
     n = n.split("(")[0]
-    for k in ("sweepk_kernel", "fused_kernel", "ib_point_kernel", "ib_ghost_kernel", "copyBuffer", "nccl", "Copy"):
+    for k in ("sweepk_kernel", "fused_kernel", "band_level_kernel", "ib_point_kernel", "ib_ghost_kernel", "copyBuffer", "nccl",
+              "Copy"):
         if k in n:
             return k
     return n[-30:]
