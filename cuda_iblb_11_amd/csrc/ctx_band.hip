@@ -149,22 +149,39 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     std::vector<int> fy0((size_t)W, INT_MAX), fy1((size_t)W, INT_MIN);
     const int zone = std::max(D, R + 2);
     bool edge_any = false;
-    for (size_t k = 0; k + 1 < xy.size(); k += 2) {
-        const int x0 = (int)std::nearbyint((double)xy[k]);
-        const int y0 = (int)std::nearbyint((double)xy[k + 1]);
-        const int ya = std::min(std::max(0, y0 - 1), ny - 1), yb = std::max(std::min(ny - 1, y0 + 1), 0);
+    // consecutive points in one column (a filament's) accumulate their rows in registers and update
+    // the column table once: per-point updates of the same few entries chain through store-to-load
+    // forwarding (768 points x K+1 iterations: 131 -> 24 us per plan on a container core)
+    int cx = INT_MIN, cy0 = 0, cy1 = 0;
+    auto flush = [&]() {
+        if (cx == INT_MIN) return;
         for (int dx = -1; dx <= 1; ++dx) {
-            const int xg = x0 + dx;  // forced global column (the spread has no periodic image)
+            const int xg = cx + dx;  // forced global column (the spread has no periodic image)
             if (xg < 0 || xg >= nx) continue;
             if (slab && !edge_any && edge_distance(c, xg) <= zone) edge_any = true;
             for (int m = -1; m <= 1; ++m) {
                 const int x = xg - c->x_begin + m * nx;
                 if (x < lo || x > hi) continue;
-                fy0[(size_t)(x + D)] = std::min(fy0[(size_t)(x + D)], std::min(ya, yb));
-                fy1[(size_t)(x + D)] = std::max(fy1[(size_t)(x + D)], std::max(ya, yb));
+                fy0[(size_t)(x + D)] = std::min(fy0[(size_t)(x + D)], cy0);
+                fy1[(size_t)(x + D)] = std::max(fy1[(size_t)(x + D)], cy1);
             }
         }
+    };
+    for (size_t k = 0; k + 1 < xy.size(); k += 2) {
+        const int x0 = (int)std::nearbyint((double)xy[k]);
+        const int y0 = (int)std::nearbyint((double)xy[k + 1]);
+        const int ya = std::min(std::max(0, y0 - 1), ny - 1), yb = std::max(std::min(ny - 1, y0 + 1), 0);
+        if (x0 == cx) {
+            cy0 = std::min(cy0, std::min(ya, yb));
+            cy1 = std::max(cy1, std::max(ya, yb));
+            continue;
+        }
+        flush();
+        cx = x0;
+        cy0 = std::min(ya, yb);
+        cy1 = std::max(ya, yb);
     }
+    flush();
     // forced column intervals with their row range, merged into patches {x0, x1, y0, y1} whose
     // trapezoids stay apart (gaps >= 2R + 8 columns)
     std::vector<std::array<int, 4>> b;
