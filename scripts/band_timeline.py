@@ -1,10 +1,12 @@
 """Per-cycle timeline of the IB band cycle from a rocprofv3 trace directory: kernels of the last
 cycles (start/end relative to the cycle's deep sweep, queue) and the host API time per cycle."""
-import csv, glob, statistics, sys
+import csv, glob, re, statistics, sys
 
 
 def short(n):
     n = n.split("(")[0]
+    if "sweepk_kernel" in n and re.search(r",\s*true\s*(,\s*\d+\s*)?>", n):
+        return "sweep_slab"  # the boundary sweeps of an RCCL slab
     for k in ("sweepk_kernel", "fused_kernel", "band_level_kernel", "ib_point_kernel", "ib_ghost_kernel", "copyBuffer", "nccl",
               "Copy"):
         if k in n:
