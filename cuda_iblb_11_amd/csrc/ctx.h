@@ -188,6 +188,7 @@ struct iblb_ctx {
     double fused_ms = 0., ib_ms = 0., halo_ms = 0., sweep_ms = 0., sweepk_ms = 0.;
     long long fused_launches = 0, fused_cells = 0, sweep_launches = 0, sweep_cells = 0, sweepk_launches = 0,
               sweepk_cells = 0;
+    long long band_cycles = 0, band_merged_cycles = 0;  // IB band cycles run (counted without events too)
     struct EvRec { int kind; size_t idx; long long cells; };
     std::vector<EvRec> ev_kind;
     std::string err;

@@ -580,6 +580,8 @@ static int band_step(iblb_ctx* c) {
     // level and the next deep sweep left ~7 us of idle queue per cycle, profiles/r03ch2)
     c->band_end = c->band_pin_ev[c->band_pin_cur];  // (the waits above took the previous cycle's)
     if ((rc = band_chain<T>(c, K, A, B, S, slab, bs, ds))) return rc;
+    c->band_cycles++;
+    if (c->band_merged && c->bf_alloc) c->band_merged_cycles++;
     c->band_run = ov;
     if (slab) {
         c->bnd_w = D > 0 ? 0 : K;  // the edge columns of g^{t+K}: the boundary sweeps' unless a trapezoid stored them
@@ -633,6 +635,14 @@ int band_release(iblb_ctx* c) {
     c->bfl_alloc = nullptr;
     c->bfd[0] = c->bfd[1] = nullptr;
     c->bfl[0] = c->bfl[1] = nullptr;
+    // the context may plan again after this: nothing above may be taken for allocated
+    c->band_pin_cap = 0;
+    c->band_pin_i = 0;
+    c->band_reserve = 0;
+    c->band_valid = false;
+    c->band_b.clear();
+    c->band_d = c->band_x = 0;
+    c->band_tab = nullptr;
     return IBLB_OK;
 }
 

@@ -737,7 +737,10 @@ int iblb_get_timing(iblb_ctx* c, iblb_timing* t, int reset) {
     t->sweepk_ms = c->sweepk_ms;
     t->sweepk_cells = c->sweepk_cells;
     t->sweepk_depth = c->sweep_depth;
+    t->band_cycles = c->band_cycles;
+    t->band_merged_cycles = c->band_merged_cycles;
     if (reset) {
+        c->band_cycles = c->band_merged_cycles = 0;
         c->fused_ms = c->ib_ms = c->halo_ms = c->sweep_ms = c->sweepk_ms = 0.;
         c->fused_launches = c->fused_cells = c->sweep_launches = c->sweep_cells = 0;
         c->sweepk_launches = c->sweepk_cells = 0;

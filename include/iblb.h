@@ -146,6 +146,10 @@ typedef struct iblb_timing {
     double    sweepk_ms;
     long long sweepk_cells;    /* lattice updates = sweepk_depth x sweepk_cells */
     long long sweepk_depth;    /* K */
+    /* IB band cycles run (ctx_band.hip), and how many of them ran the merged chain; counted
+     * whether or not profiling events are on */
+    long long band_cycles;
+    long long band_merged_cycles;
 } iblb_timing;
 
 /* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */

@@ -1,0 +1,9 @@
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/r04a
+mkdir -p $OUT
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
+grep smoke $OUT/smoke.log
+timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+TAG=r04a WIDTHS=512 bash scripts/r03_scaling.sh

@@ -305,6 +305,50 @@ def test_rccl_slab_band_cycle_threads(gpu, n, precision, mode):
     test_rccl_slab_path_threads(gpu, n, mode, precision, 1, 1, 5, nx=48 * n)
 
 
+@pytest.mark.parametrize("n,precision,merge", [(2, "f64", "0"), (4, "f32", "0"), (8, "f32", "0"), (3, "f64", "2")])
+def test_rccl_slab_band_cycle_threads_chain(gpu, n, precision, merge, monkeypatch):
+    """Mode 3 (filaments across every slab edge, band cycle on every rank) with the band chain
+    forced: IBLB_BAND_MERGE=0 runs the chained chain (2K launches: IB, then the level) that the
+    48N-column slabs never select by themselves, 2 the merged chain."""
+    monkeypatch.setenv("IBLB_BAND_MERGE", merge)
+    test_rccl_slab_path_threads(gpu, n, "3", precision, 1, 1, 5, nx=48 * n)
+
+
+@pytest.mark.parametrize("n,workload,merge", [(2, "K4", None), (4, "K4", None), (8, "K4", None),
+                                              (2, "K5", None), (4, "K5", None), (8, "K5", None),
+                                              (8, "K5", "0"), (2, "K5", "2")])
+def test_full_size_decomposed(gpu, n, workload, merge):
+    """BASELINE configs 4 and 5 decomposed at their real size, 8192 x 2048 over 2 / 4 / 8 ranks
+    (mock RCCL: ranks as threads on one GPU), 21 iterations in bulk calls (boot + 4 cycles), against
+    the lone slab and the oracle (tests/mock_rccl/run_full.py).  K4 f64: bit-identical to the lone
+    slab, <= 1e-9 vs the oracle.  K5 f32 + 64 filaments x 96 points on every slab edge (x = 0
+    included), moving every iteration: the IB band cycle on every rank, <= 1e-4 vs the oracle.
+    The band chain flavour: auto picks the chained chain on the 4096-column f32 slabs of N = 2 (their
+    deep sweep outlasts a chain) and the merged chain on the 2048 / 1024-column slabs of N = 4 / 8;
+    the last two cases force the other flavour."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ)
+    env.pop("IBLB_BAND_MERGE", None)
+    if merge is not None:
+        env["IBLB_BAND_MERGE"] = merge
+    cmd = [sys.executable, os.path.join(here, "mock_rccl", "run_full.py"), str(n), workload]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines, p.stdout + p.stderr[-3000:]
+    res = json.loads(lines[-1])
+    print(json.dumps(res))
+    assert p.returncode == 0 and res["ok"], (res, p.stderr[-2000:])
+    if workload == "K5":
+        merged = [rk["band_merged_cycles"] for rk in res["ranks"]]
+        cycles = [rk["band_cycles"] for rk in res["ranks"]]
+        expect_merged = merge == "2" or (merge is None and n >= 4)
+        assert merged == (cycles if expect_merged else [0] * n), res["ranks"]
+
+
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_reference_cilia_scenario(gpu, oracle, precision):
     """The reference's own scenario (main.cu defaults: 6 cilia, c_space 48 -> 288 x 192, T = 1e5),
