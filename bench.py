@@ -4,9 +4,10 @@
 
 One step = one reference iteration (main.cu:852-909) over the whole 4096 x 4096 channel
 (periodic x, bounce-back / mirror walls, TRT + Guo forcing, uniform body force, no IB): one
-two-iteration sweep launch (pull-stream + collide twice, lbm_sweep.hip) per two steps and slab.
-N > 1: x-slab decomposition of the SAME 4096^2 lattice (strong scaling), one process per GPU,
-2-column halo via RCCL beside the interior sweep; `--scaling weak`
+deep sweep launch (pull-stream + collide K = 5 times, intermediate states in registers,
+lbm_sweep_impl.h) per five steps and slab.  N > 1: x-slab decomposition of the SAME 4096^2
+lattice (strong scaling), one process per GPU; per 5-iteration cycle a K-column ghost exchange
+via RCCL and the boundary sweeps run on a comm stream beside the interior sweep; `--scaling weak`
 gives every rank the configured width instead ((nx*N) x ny).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f64|f32] [--nx 4096 --ny 4096]
@@ -43,7 +44,7 @@ WORKLOADS = {
     "K2": (2048, 2048, "f64", None, "K2: 2048x2048 D2Q9 channel, no IB"),
     "K3": (2048, 2048, "f64", "filament", "K3: 2048x2048 channel + one 256-point filament"),
     "K4": (8192, 2048, "f64", None, "K4: 8192x2048 channel, no IB"),
-    "K5": (8192, 2048, "f32", "array", "K5: 8192x2048 channel + 64 filaments x 96 points, one on every slab edge"),
+    "K5": (8192, 2048, "f32", "array", "K5: 8192x2048 channel + 64 filaments x 96 points"),
 }
 
 
@@ -255,6 +256,10 @@ def main():
     from cuda_iblb_11_amd import workloads as W
 
     wnx, wny, wprec, wpts, wdesc = WORKLOADS[a.workload]
+    if wpts == "array":
+        wdesc += (", one on every slab edge (x = 0 included)" if a.filament_offset == 0.0 else
+                  ", every filament mid-slab" if a.filament_offset == 0.5 else
+                  f", filament m at (m + {a.filament_offset}) * 128 columns")
     nx, ny = a.nx or wnx, a.ny or wny
     if a.scaling == "weak":
         nx *= world
@@ -359,9 +364,17 @@ def main():
         launch_ms = tm["sweepk_ms"] / tm["sweepk_launches"]
         cells_per_launch = tm["sweepk_cells"] // tm["sweepk_launches"]
         iters_per_launch = sweep
-    if a.no_profile_events:  # nothing timed per launch: name the kernel the configuration runs
-        sweep = max(2, min(6, int(os.environ.get("IBLB_SWEEP_DEPTH", "5"))))
-        iters_per_launch = sweep
+    if a.no_profile_events:  # nothing timed per launch: name the kernel from what ran
+        # (the band-cycle counter is kept without events; a deep run without IB shows as no
+        # one-step launches at all, since only the boot iteration and remainders are one-step)
+        depth = int(tm["sweepk_depth"])
+        if tm["band_cycles"] > 0 or (ns == 0 and os.environ.get("IBLB_SWEEP", "1") != "0" and depth >= 3):
+            sweep = depth
+        elif ns == 0 and os.environ.get("IBLB_SWEEP", "1") != "0":
+            sweep = 2
+        else:
+            sweep = False
+        iters_per_launch = sweep or 1
         launch_ms, cells_per_launch = 0.0, 0
     if distributed:
         sl = torch.tensor([launch_ms], dtype=torch.float64, device=red_dev)
@@ -416,6 +429,9 @@ def main():
                             + ("; IB band cycle: columns within K-1 of a forced column one iteration per launch, "
                                "the rest in the deep sweep" if ns and tm["sweepk_launches"] else ""),
                 "nx": nx, "ny": ny, "global_cells": cells, "ib_points": ns,
+                **({"filament_offset": a.filament_offset} if wpts == "array" else {}),
+                **({"band_cycles": int(tm["band_cycles"]), "band_merged_cycles": int(tm["band_merged_cycles"])}
+                   if ns else {}),
                 "parallelism": f"x-slab x{world}" + (" (RCCL halo)" if world > 1 and not rehearsal else "")
                                + (" (RCCL self-ring rehearsal)" if a.rccl_self and world == 1 else "")
                                + (" (same-device rehearsal: every rank a self ring over its slab on GPU 0)"

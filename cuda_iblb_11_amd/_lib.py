@@ -106,6 +106,7 @@ _SIGS = {
     "iblb_get_lagrangian_force": ([_vp, _vp], C.c_int),
     "iblb_get_flux": ([_vp, C.POINTER(C.c_double)], C.c_int),
     "iblb_get_step": ([_vp, C.POINTER(C.c_longlong)], C.c_int),
+    "iblb_count_nonfinite": ([_vp, C.POINTER(C.c_longlong)], C.c_int),
     "iblb_set_profiling": ([_vp, C.c_int], C.c_int),
     "iblb_get_timing": ([_vp, C.POINTER(Timing), C.c_int], C.c_int),
     "iblb_get_stream": ([_vp, C.POINTER(_vp)], C.c_int),

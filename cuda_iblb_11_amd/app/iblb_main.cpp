@@ -303,6 +303,16 @@ int main(int argc, char* argv[]) {
 
         //----------------------------DATA OUTPUT------------------------------ (main.cu:938-1005)
         if (it % INTERVAL == 0) {
+            // not in the reference (it writes NaN fields on): a diverged run stops here, loudly,
+            // on every rank (the count is collective)
+            long long bad = 0;
+            if ((rc = iblb_count_nonfinite(ctx, &bad))) return die(ctx, rc, "iblb_count_nonfinite");
+            if (bad > 0) {
+                cerr << "IBLB: the run diverged: " << bad << " non-finite populations at iteration " << it
+                     << " (output and further iterations skipped)" << endl;
+                iblb_destroy(ctx);
+                return 3;
+            }
             if (BigData) {
                 if ((rc = iblb_gather_macro(ctx, 0, lead ? rho.data() : nullptr, lead ? u.data() : nullptr)))
                     return die(ctx, rc, "iblb_gather_macro");

@@ -378,8 +378,9 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
 // ghost edge (the launch after a level clears that level's force at its own entries, one column
 // narrower: the dropped column lies inside the garbage frontier, at level j columns up to
 // -D+2+3j are garbage, §5 of DESIGN.md), and level K-2 only where the last level's cells and the
-// nodes of its force pull: columns -3 .. ncol+2 (a point forcing column 0 has nodes from -1, their
-// pulls from -2, the collides of those from -3); the last launch clears those outside its own.
+// nodes of its force pull: columns -3 .. ncol+2 (a point that forces column 0 has x0 >= -1, so its
+// nodes start at x0-1 >= -2; their pulls reach -3, where the level's collide is recomputed, so the
+// level's force is needed from column -3); the last launch clears those outside its own.
 static void force_clip(const iblb_ctx* c, int j, bool merged, int* clo, int* chi) {
     const int K = c->sweep_depth, D = c->band_d, n = c->ncol;
     if (j == K - 1) {

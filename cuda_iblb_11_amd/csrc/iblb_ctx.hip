@@ -703,6 +703,26 @@ int iblb_get_flux(iblb_ctx* c, double* Q) {
     return IBLB_OK;
 }
 
+int iblb_count_nonfinite(iblb_ctx* c, long long* count) {
+    if (!c || !count) return IBLB_ERR_ARG;
+    int rc = check_ready(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    if ((rc = band_join(c)) || (rc = join_comm(c))) return rc;
+    HIP_TRY(c, hipMemsetAsync(c->d_Q + 1, 0, sizeof(double), c->stream));
+    if (is_f64(c)) HIP_TRY(c, launch_count_nonfinite<double>(gptr<double>(c, c->cur), c->L, c->d_Q + 1, c->stream));
+    else HIP_TRY(c, launch_count_nonfinite<float>(gptr<float>(c, c->cur), c->L, c->d_Q + 1, c->stream));
+    if (rccl_multi(c)) {
+        if ((rc = rccl_order(c, c->stream))) return rc;
+        NCCL_TRY(c, ncclAllReduce(c->d_Q + 1, c->d_Q + 1, 1, ncclFloat64, ncclSum, c->comm, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    double n = 0.;
+    HIP_TRY(c, hipMemcpy(&n, c->d_Q + 1, sizeof(double), hipMemcpyDeviceToHost));
+    *count = (long long)n;
+    return IBLB_OK;
+}
+
 int iblb_get_step(iblb_ctx* c, long long* steps) {
     if (!c || !steps) return IBLB_ERR_ARG;
     *steps = c->t;

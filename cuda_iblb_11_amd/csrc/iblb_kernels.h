@@ -139,6 +139,11 @@ template <typename T>
 hipError_t launch_flux(const T* g, Layout L, Halo<T> H, const double* fdense, long fplane,
                        double gx, double gy, int xc, double flux_norm, double* out, hipStream_t s);
 
+// Non-finite stored populations of the slab's own cells (rows < ny, all nine planes), added to
+// *count (one double: an exact integer up to 2^53).
+template <typename T>
+hipError_t launch_count_nonfinite(const T* g, Layout L, double* count, hipStream_t s);
+
 // Reference AoS populations [9*j+i] -> slab planes (deviation form for float).
 template <typename T>
 hipError_t launch_pop_in(const double* f, T* g, Layout L, hipStream_t s);

@@ -354,6 +354,24 @@ hipError_t launch_flux(const T* g, Layout L, Halo<T> H, const double* fdense, lo
     return hipGetLastError();
 }
 
+// one block per (column, plane): the rows of one plane of one column are contiguous
+template <typename T>
+__global__ void count_nonfinite_kernel(const T* __restrict__ g, Layout L, double* count) {
+    const int xc = (int)blockIdx.x, k = (int)blockIdx.y;
+    const T* p = g + (long)xc * L.col + (long)k * L.plane;
+    int bad = 0;
+    for (int y = threadIdx.x; y < L.ny; y += blockDim.x) bad += !isfinite(p[y]);
+    const double n = wave_sum((double)bad);
+    if ((threadIdx.x & 63) == 0 && n > 0.) atomicAdd(count, n);
+}
+
+template <typename T>
+hipError_t launch_count_nonfinite(const T* g, Layout L, double* count, hipStream_t s) {
+    if (L.ncol <= 0) return hipSuccess;
+    count_nonfinite_kernel<T><<<dim3((unsigned)L.ncol, 9), 256, 0, s>>>(g, L, count);
+    return hipGetLastError();
+}
+
 // ---- layout conversion ------------------------------------------------------------------
 template <typename T>
 __global__ void pop_in_kernel(const double* __restrict__ f, T* __restrict__ g, Layout L) {
@@ -411,7 +429,8 @@ hipError_t launch_field_out(const double* lay, double* ref, Layout L, int ncomp,
     template hipError_t launch_pop_out<T>(const T*, Layout, Halo<T>, double*, int, hipStream_t);                     \
     template hipError_t launch_flux<T>(const T*, Layout, Halo<T>, const double*, long, double, double, int,      \
                                        double, double*, hipStream_t);                                           \
-    template hipError_t launch_pop_in<T>(const double*, T*, Layout, hipStream_t);
+    template hipError_t launch_pop_in<T>(const double*, T*, Layout, hipStream_t);                                \
+    template hipError_t launch_count_nonfinite<T>(const T*, Layout, double*, hipStream_t);
 
 IBLB_INST(double)
 IBLB_INST(float)

@@ -246,6 +246,13 @@ class Lattice:
         self._check(self._lib.iblb_get_step(self._h, C.byref(n)))
         return n.value
 
+    def count_nonfinite(self) -> int:
+        """NaN / Inf stored populations of the current state (whole lattice; collective in an
+        RCCL group)."""
+        n = C.c_longlong(0)
+        self._check(self._lib.iblb_count_nonfinite(self._h, C.byref(n)))
+        return n.value
+
     # -- timing -----------------------------------------------------------------------------
     def set_profiling(self, on: bool = True) -> None:
         self._check(self._lib.iblb_set_profiling(self._h, 1 if on else 0))

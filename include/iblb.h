@@ -217,6 +217,10 @@ int iblb_get_lagrangian_force(iblb_ctx* ctx, float* F_s);
  * is the sum over all ranks; with a local group it is this slab's share. */
 int iblb_get_flux(iblb_ctx* ctx, double* Q);
 int iblb_get_step(iblb_ctx* ctx, long long* steps);
+/* Non-finite (NaN / Inf) stored populations of the current state, counted over every cell
+ * of the lattice (summed over the ranks of an RCCL group: collective).  The driver checks it
+ * at every output iteration (the reference's penalty IB can diverge). */
+int iblb_count_nonfinite(iblb_ctx* ctx, long long* count);
 
 /* Timing: when enabled every collide-stream launch is bracketed by HIP events on the
  * stream it runs on; iblb_get_timing() returns the sums (and resets them if reset). */
@@ -228,9 +232,12 @@ int iblb_get_stream(iblb_ctx* ctx, void** stream);
 int iblb_synchronize(iblb_ctx* ctx);
 
 /* ---- x-slab decomposition -------------------------------------------------------
- * Slabs are ordered along x (periodic).  A slab exchanges a one-column halo with its
- * two neighbours every step: populations {1,5,8} of its last column go right,
- * {3,6,7} of its first column go left.
+ * Slabs are ordered along x (periodic).  Every population buffer of a slab holds ghost
+ * columns on both sides (3K per side, K = IBLB_SWEEP_DEPTH); a halo exchange of depth d
+ * sends the d whole edge columns of the current state to each neighbour and receives the
+ * neighbours' into the ghost columns, in place (no packing): d = 1 for a one-step
+ * iteration, 3 when an owed IB force is evaluated from the ghosts, K per K-iteration deep
+ * cycle, 3K per IB band cycle whose trapezoids cross a slab edge.
  *
  * Local group: n contexts of ONE process (any devices with peer access) linked
  * left-to-right; iblb_group_step() advances them together.  Synchronous transport,

@@ -1,0 +1,166 @@
+"""The GPU's f32 collide-stream iteration emulated in numpy (test infrastructure): every operation
+of relax_cell<float, DEV = true> (csrc/iblb_device.h) in its order, each result rounded to float32,
+fused multiply-adds evaluated in float64 and rounded once to float32 (the product of two float32
+values is exact in float64, so only a sum that lands within 2^-29 of a float32 tie can round
+differently from the hardware's fma), the collide constants folded in float32 as make_kbase /
+make_kforce fold them.  Storage: deviations h = f - w_i, pull streaming with the reference's wall
+rules (iblb_device.h:14-19).
+
+Where tests/f32_model.py is an independent float32 restatement of the reference algorithm (the
+precision's floor), this model is the GPU's own arithmetic on the CPU: its distance from the f64
+oracle after n iterations says what the kernels' operation order costs in float32, without a GPU.
+`variant` selects alternative orders of the same algebra: "gpu" as the kernels
+compute it; "rho_free" computes the odd equilibrium part from the momentum rho u = m + F/2 directly
+and rho-scaled constants as c + (rho - 1) c, so the rounded rho = 1 + (rho - 1) enters only 1/rho.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+f32, f64 = np.float32, np.float64
+C_S = 0.57735  # LatticeBoltzmann.cu:11
+CX = np.array([0, 1, 0, -1, 0, 1, -1, -1, 1])
+CY = np.array([0, 0, 1, 0, -1, 1, 1, -1, -1])
+WD = np.array([4 / 9] + [1 / 9] * 4 + [1 / 36] * 4)
+PA, PB = (1, 2, 5, 6), (3, 4, 7, 8)  # pairs (iblb_device.h pair_a / pair_b)
+
+
+def fma(a, b, c):
+    return (np.asarray(a, f64) * np.asarray(b, f64) + np.asarray(c, f64)).astype(f32)
+
+
+def kconst(tau, tau2, gx, gy):
+    """make_kbase<float> / make_kforce<float> (iblb_device.h:167-210), contraction off."""
+    op, om = f32(1.0 / tau), f32(1.0 / tau2)
+    kk = f32(1.0 - 1.0 / (2.0 * tau))
+    ics2, ics4 = f32(1.0 / (C_S * C_S)), f32(1.0 / (C_S * C_S * C_S * C_S))
+    a2 = f32(1.0 / (2.0 * C_S * C_S * C_S * C_S))
+    k = {"omp": f32(1) - op, "opwr": op * f32(4.0 / 9), "a1": f32(1.0 / (2.0 * C_S * C_S))}
+    for cl, w in ((0, f32(1.0 / 9)), (1, f32(1.0 / 36))):
+        k[f"opw{cl}"] = op * w
+        k[f"oqa{cl}"] = k[f"opw{cl}"] * a2
+        k[f"omwi2{cl}"] = om * w * ics2
+        kw = kk * w
+        k[f"kwi4{cl}"] = kw * ics4
+        k[f"kwi2{cl}"] = kw * ics2
+        k[f"nck{cl}"] = -(ics2 * kw)
+    k["hs"] = f32(0.5) * k["omp"]
+    k["hd"] = f32(0.5) * (f32(1) - om)
+    Fx, Fy = f32(gx), f32(gy)
+    k["Fx"], k["Fy"], k["hFx"], k["hFy"] = Fx, Fy, f32(0.5) * Fx, f32(0.5) * Fy
+    cF = (Fx, Fy, Fx + Fy, Fy - Fx)
+    for p in range(4):
+        cl = 0 if p < 2 else 1
+        k[f"hE{p}"] = cF[p] * k[f"kwi4{cl}"]
+        k[f"gO{p}"] = cF[p] * k[f"kwi2{cl}"]
+    return k
+
+
+def relax(h, k, variant="gpu"):
+    """relax_cell<float, true> on arrays h[9, ...] of pulled deviations; returns h1."""
+    s = [h[PA[p]] + h[PB[p]] for p in range(4)]
+    d = [h[PA[p]] - h[PB[p]] for p in range(4)]
+    sm = h[0] + ((s[0] + s[1]) + (s[2] + s[3]))
+    mx = d[0] + (d[2] - d[3])
+    my = d[1] + (d[2] + d[3])
+    rho = f32(1) + sm
+    inv = (f64(1) / rho.astype(f64)).astype(f32)  # v_rcp_f32 + one Newton step
+    jx, jy = mx + k["hFx"], my + k["hFy"]
+    ux, uy = jx * inv, jy * inv
+    usq = fma(uy, uy, ux * ux)
+    uF = fma(uy, k["Fy"], ux * k["Fx"])
+    base = (-usq) * k["a1"]
+    rb = fma(rho, base, sm)
+    out = np.empty_like(h)
+    out[0] = fma(k["omp"], h[0], rb * k["opwr"])
+    P, Qa, Rm = [], [], []
+    for cl in (0, 1):
+        P.append(fma(rb, k[f"opw{cl}"], uF * k[f"nck{cl}"]))
+        if variant == "rho_free":
+            Qa.append(fma(sm, k[f"oqa{cl}"], k[f"oqa{cl}"]))
+        else:
+            Qa.append(rho * k[f"oqa{cl}"])
+            Rm.append(rho * k[f"omwi2{cl}"])
+    for p in range(4):
+        cl = 0 if p < 2 else 1
+        cu = (ux, uy, ux + uy, uy - ux)[p]
+        E = fma(cu, fma(Qa[cl], cu, k[f"hE{p}"]), P[cl])
+        if variant == "rho_free":  # rho (c.u) = c.(m + F/2): no rho, no 1/rho in the odd part
+            cj = (jx, jy, jx + jy, jy - jx)[p]
+            O = fma(k[f"omwi2{cl}"], cj, k[f"gO{p}"])
+        else:
+            O = fma(Rm[cl], cu, k[f"gO{p}"])
+        A = fma(s[p], k["hs"], E)
+        B = fma(d[p], k["hd"], O)
+        out[PA[p]] = A + B
+        out[PB[p]] = A - B
+    return out
+
+
+def pull(g):
+    """f^t from the post-collision state g[9, ny, nx] (periodic x, bounce-back at y = 0, same-cell
+    mirror at y = ny-1)."""
+    f = np.empty_like(g)
+    for i in range(9):
+        src = np.roll(g[i], CX[i], axis=1)
+        if CY[i] == 0:
+            f[i] = src
+        elif CY[i] == 1:
+            f[i, 1:] = src[:-1]
+        else:
+            f[i, :-1] = src[1:]
+    for k_, kk in ((2, 4), (5, 7), (6, 8)):
+        f[k_, 0] = g[kk, 0]
+    for k_, kk in ((4, 2), (8, 5), (7, 6)):
+        f[k_, -1] = g[kk, -1]
+    return f
+
+
+class F32GpuChannel:
+    """No-IB channel from rho, u (reference layout); the boot iteration in float64 (the GPU boots
+    from the given double fields), then float32 iterations in the kernels' order."""
+
+    def __init__(self, nx, ny, tau, tau2, rho, u, body_force, variant="gpu"):
+        self.nx, self.ny, self.variant = nx, ny, variant
+        self.k = kconst(tau, tau2, *body_force)
+        rho = np.asarray(rho, f64).reshape(ny, nx)
+        u = np.asarray(u, f64)
+        ux, uy = u[:nx * ny].reshape(ny, nx), u[nx * ny:].reshape(ny, nx)
+        gx, gy = body_force
+        cs2 = C_S * C_S
+        # boot: f^0 = feq(rho, u), collided with rho, u, the body force (equilibrium + Guo, TRT)
+        usq = ux * ux + uy * uy
+        feq = np.empty((9, ny, nx))
+        Fi = np.empty((9, ny, nx))
+        kg = 1.0 - 1.0 / (2.0 * tau)
+        for i in range(9):
+            cu = CX[i] * ux + CY[i] * uy
+            feq[i] = rho * WD[i] * (1 + cu / cs2 + cu * cu / (2 * cs2 * cs2) - usq / (2 * cs2))
+            vx = (CX[i] - ux) / cs2 + cu / (cs2 * cs2) * CX[i]
+            vy = (CY[i] - uy) / cs2 + cu / (cs2 * cs2) * CY[i]
+            Fi[i] = kg * WD[i] * (vx * gx + vy * gy)
+        g = np.empty_like(feq)
+        g[0] = feq[0]  # f = feq: the collision leaves f0, adds no F_0
+        for a, b in zip(PA, PB):
+            g[a] = feq[a] + Fi[a]
+            g[b] = feq[b] + Fi[b]
+        self.g = (g - WD[:, None, None]).astype(f32)
+        self.booted = False  # the boot collide above is the first iteration
+
+    def step(self, n=1):
+        for _ in range(n):
+            if not self.booted:
+                self.booted = True
+                continue
+            self.g = relax(pull(self.g), self.k, self.variant)
+
+    def macro(self):
+        """rho (= 1 + the deviation sum), u = (m + F/2)/rho, in float64 from the stored f32 state."""
+        f = pull(self.g).astype(f64)
+        dr = f.sum(axis=0)
+        rho = 1.0 + dr
+        mx = f[1] - f[3] + f[5] - f[6] - f[7] + f[8]
+        my = f[2] - f[4] + f[5] + f[6] - f[7] - f[8]
+        ux = (mx + 0.5 * float(self.k["Fx"])) / rho
+        uy = (my + 0.5 * float(self.k["Fy"])) / rho
+        return rho.ravel(), np.concatenate([ux.ravel(), uy.ravel()])

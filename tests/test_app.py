@@ -159,3 +159,15 @@ def test_app_restart_continues_the_run(gpu, tmp_path, expected):
     last_got = read(tmp_path, M.paths(p)["flux"]).strip().split("\n")[-1]
     last_exp = files[M.paths(p)["flux"]].strip().split("\n")[-1]
     compare_text(last_got, last_exp, 1e-5, "final flux")
+
+
+@pytest.mark.gpu
+def test_app_stops_a_diverged_run(gpu, tmp_path):
+    """The reference's own scenario diverges by iteration ~40 (penalty IB gain) and
+    the reference writes NaN fields on; the driver checks the populations at every output
+    iteration (iblb_count_nonfinite, collective) and stops with status 3 instead."""
+    args = ARGS[:6] + ["0.001", "10"] + ARGS[8:]  # 100 iterations, output every 10
+    assert M.params(args)["ITERATIONS"] == 100
+    r = run_app(args, tmp_path)
+    assert r.returncode == 3, r.stdout + r.stderr
+    assert "the run diverged" in r.stderr, r.stderr

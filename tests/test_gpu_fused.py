@@ -251,6 +251,23 @@ def test_k3_full_size_filament(gpu, oracle):
     oracle.set_threads(1)
 
 
+def test_count_nonfinite(gpu):
+    """iblb_count_nonfinite: zero on a healthy state (lone slab and after steps), every population
+    of a NaN cell, f64 and f32."""
+    from cuda_iblb_11_amd import workloads as W
+    for prec in ("f64", "f32"):
+        rho, u = W.perturbed_state(64, 32, 3)
+        lat = gpu.Lattice(64, 32, W.TAU, W.TAU2, precision=prec, body_force=W.BODY_FORCE)
+        lat.set_state(rho, u)
+        assert lat.count_nonfinite() == 0
+        lat.step(7)
+        assert lat.count_nonfinite() == 0
+        rho[5 * 64 + 17] = np.nan
+        lat.set_state(rho, u)
+        assert lat.count_nonfinite() == 9
+        lat.close()
+
+
 def test_errors_are_loud(gpu):
     from cuda_iblb_11_amd import workloads as W
     lat = gpu.Lattice(16, 8, W.TAU, W.TAU2)
