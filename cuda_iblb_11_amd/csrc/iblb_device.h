@@ -209,9 +209,14 @@ __host__ __device__ inline KForce<R> make_kforce(const KBase<R>& b, R Fx, R Fy) 
     return k;
 }
 
-template <typename R, bool DEV>
+// JM (the f32 path): the odd equilibrium part from the momentum j = rho u = m + F/2 itself,
+// w- feq- = (w- w / cs^2) c.j, and the rho-scaled constants as c + (rho - 1) c: the density rounded
+// to float32 (rho = 1 + (rho - 1) keeps ~7 digits of a deviation ~1e-5) then enters only through
+// 1/rho.  Measured on the K1 1000-iteration f32 run in the CPU emulation of this arithmetic
+// (tests/f32_gpu_model.py): rho - 1 1.8e-4 -> 7.9e-5, u_y 8.9e-5 -> 3.6e-5.
+template <typename R, bool DEV, bool JM = false>
 __device__ __forceinline__ void collide_sd(R f[9], const R s[4], const R d[4], R rho, R sum, R ux, R uy,
-                                           const KBase<R>& b, const KForce<R>& k) {
+                                           const KBase<R>& b, const KForce<R>& k, R jx = 0, R jy = 0) {
 #pragma clang fp contract(on)  // fuse within a statement only: the same FMAs in every kernel
     const R usq = ux * ux + uy * uy;
     const R uF = ux * k.Fx + uy * k.Fy;
@@ -226,8 +231,13 @@ __device__ __forceinline__ void collide_sd(R f[9], const R s[4], const R d[4], R
 #pragma unroll
     for (int cl = 0; cl < 2; ++cl) {
         P[cl] = fmaR(rb, b.opw[cl], uF * b.nck[cl]);
-        Qa[cl] = rho * b.oqa[cl];
-        Rm[cl] = rho * b.omwi2[cl];
+        if (JM) {
+            Qa[cl] = fmaR(sum, b.oqa[cl], b.oqa[cl]);
+            Rm[cl] = b.omwi2[cl];
+        } else {
+            Qa[cl] = rho * b.oqa[cl];
+            Rm[cl] = rho * b.omwi2[cl];
+        }
     }
     // per pair: the even part A = hs s + E and the odd part B = hd d + O of the post-collision
     // pair, f_a = A + B, f_b = A - B (7-8 fp64 operations per pair; the kernels are issue-bound
@@ -238,7 +248,8 @@ __device__ __forceinline__ void collide_sd(R f[9], const R s[4], const R d[4], R
         const int cl = p < 2 ? 0 : 1;
         const R cu = p == 0 ? ux : (p == 1 ? uy : (p == 2 ? ux + uy : uy - ux));  // c_a . u
         const R E = fmaR(cu, fmaR(Qa[cl], cu, k.hE[p]), P[cl]);
-        const R O = fmaR(Rm[cl], cu, k.gO[p]);
+        const R cj = JM ? (p == 0 ? jx : (p == 1 ? jy : (p == 2 ? jx + jy : jy - jx))) : cu;  // c_a . j
+        const R O = fmaR(Rm[cl], cj, k.gO[p]);
         const R A = fmaR(s[p], b.hs, E);
         const R B = fmaR(d[p], b.hd, O);
         f[a] = A + B;
@@ -292,9 +303,10 @@ __device__ __forceinline__ R relax_cell(R f[9], const KBase<R>& b, const KForce<
     const R my = d[1] + (d[2] + d[3]);
     const R rho = DEV ? (R)1 + sum : sum;
     const R inv = recip(rho);
-    const R ux = (mx + k.hFx) * inv;
-    const R uy = (my + k.hFy) * inv;
-    collide_sd<R, DEV>(f, s, d, rho, sum, ux, uy, b, k);
+    const R jx = mx + k.hFx, jy = my + k.hFy;
+    const R ux = jx * inv;
+    const R uy = jy * inv;
+    collide_sd<R, DEV, DEV>(f, s, d, rho, sum, ux, uy, b, k, jx, jy);
     return ux;
 }
 

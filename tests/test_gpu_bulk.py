@@ -119,11 +119,13 @@ def test_m_bulk_f32(gpu, oracle, threads):
 
 
 def test_k1_1000_steps_bulk_f32(gpu, oracle, threads):
-    """f32 over the longest horizon: 128^2, 1000 iterations in one call (199 deep launches).
-    By then rho - 1 has decayed to ~1e-5 while f32 rounding keeps adding ~1e-12 per cell and
-    iteration, so the 1e-4 bound on rho - 1 is below what float32 arithmetic can hold: a plain
-    numpy float32 restatement of the same iteration (tests/f32_model.py) lands at 1.5e-4 on
-    rho - 1 and u_y.  Bound: 1e-4, or twice that f32 floor where the floor itself exceeds it."""
+    """f32 over the longest horizon: 128^2, 1000 iterations in one call (199 deep launches), within
+    the north star's 1e-4 on rho - 1, u_x, u_y (each normalised by its own max).  By then rho - 1
+    has decayed to ~1e-5 while f32 rounding keeps adding ~1e-12 per cell and iteration; a plain
+    numpy float32 restatement (tests/f32_model.py) lands at 1.5e-4 on rho - 1 and u_y.  The kernels'
+    f32 collide takes the odd equilibrium part from the momentum and never multiplies by the
+    float32-rounded rho (iblb_device.h collide_sd, JM): 7.9e-5 / 3.6e-5 in the CPU emulation of the
+    same arithmetic (tests/f32_gpu_model.py; the round-3 order measured 1.8e-4 on rho - 1)."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from f32_model import F32Channel
@@ -139,11 +141,7 @@ def test_k1_1000_steps_bulk_f32(gpu, oracle, threads):
     floor = {"rho-1": rel(mr - 1, sim.rho - 1), "ux": rel(mu[:N], sim.u[:N]), "uy": rel(mu[N:], sim.u[N:])}
     _record("K1_128_f32_1000", r)
     _record("K1_128_f32_1000_numpy_f32_floor", floor)
-    for k, v in floor.items():
-        assert r[k] <= max(TOL32, 2 * v), (k, r, floor)
-    # a fixed ceiling as well (recorded: rho-1 1.8e-4, u_x 1.2e-6, u_y 8.4e-5, profiles/r03z/parity_f32.json):
-    # the model-relative bound alone would loosen with any error added to the model itself
-    assert max(r.values()) <= 2e-4, r
+    assert max(r["rho-1"], r["ux"], r["uy"]) <= TOL32, (r, floor)
     assert abs(lat.flux - sim.flux) <= TOL32 * abs(sim.flux)
 
 

@@ -324,3 +324,30 @@ def test_f32_model_tracks_oracle(oracle):
     rel = lambda a, b: float(np.max(np.abs(a - b)) / np.max(np.abs(b)))
     assert rel(r - 1, sim.rho - 1) < 5e-6
     assert rel(v[:n], sim.u[:n]) < 5e-6 and rel(v[n:], sim.u[n:]) < 5e-6
+
+
+def test_f32_gpu_order_over_1000_iterations(oracle):
+    """tests/f32_gpu_model.py (the kernels' f32 arithmetic, op for op, on the CPU) against the oracle
+    on the K1 horizon (128^2, 1000 iterations).  The round-3 order ("r03": rho * constant and
+    rho (c.u) with the float32-rounded rho) lands where the GPU's round-3 f32 path was measured
+    (rho - 1 1.8e-4, u_x 1.2e-6, u_y 8.4e-5, profiles/r03z/parity_f32.json): the cause of the gap to
+    the 1e-4 bound.  The kernels' current order (odd part from the momentum, rho-scaled constants
+    as c + (rho - 1) c) holds every field within 1e-4."""
+    from cuda_iblb_11_amd import workloads as W
+    from f32_gpu_model import F32GpuChannel
+    nx = ny = 128
+    rho, u = W.perturbed_state(nx, ny, 31)
+    oracle.set_threads(min(8, os.cpu_count() or 1))
+    sim = oracle.Simulation(nx, ny, W.TAU, W.TAU2, rho=rho, u=u, body_force=W.BODY_FORCE)
+    sim.step(1000)
+    n = nx * ny
+    err = {}
+    for v in ("r03", "gpu"):
+        m = F32GpuChannel(nx, ny, W.TAU, W.TAU2, rho, u, W.BODY_FORCE, variant=v)
+        m.step(1000)
+        r, uu = m.macro()
+        err[v] = {"rho-1": float(np.max(np.abs(r - sim.rho)) / np.max(np.abs(sim.rho - 1))),
+                  "ux": float(np.max(np.abs(uu[:n] - sim.u[:n])) / np.max(np.abs(sim.u[:n]))),
+                  "uy": float(np.max(np.abs(uu[n:] - sim.u[n:])) / np.max(np.abs(sim.u[n:])))}
+    assert 1.5e-4 <= err["r03"]["rho-1"] <= 2.1e-4 and 5e-5 <= err["r03"]["uy"] <= 1.2e-4, err
+    assert max(err["gpu"].values()) <= 1e-4, err
