@@ -339,7 +339,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->deep_vs = (int)env_long("IBLB_DEEP_VS", 2);
     // f32: the wall split (variant bit 1, three waves per SIMD: M f32 0.318 vs 0.341 ms per launch,
     // profiles/r03sp)
-    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 1 : 3);
+    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 1 : 11);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_merge = (int)env_long("IBLB_BAND_MERGE", 1);

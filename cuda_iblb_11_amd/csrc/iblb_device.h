@@ -282,6 +282,61 @@ __device__ __forceinline__ float recip(float x) {
     return __builtin_fmaf(r, __builtin_fmaf(-x, r, 1.f), r);
 }
 
+// The f32 (deviation storage) collide with explicit operations only (no contraction left to the
+// compiler), on one cell (V = float) or on the two cells of a lane at once (V = f32x2: every
+// operation one packed VALU instruction, v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32, constants
+// broadcast from scalar registers).  The same operations in the same order per element, so both
+// round every cell identically: the deep sweep's packed walk stays bit-identical to the one-step
+// kernels.  rho-free odd part and rho-scaled constants as collide_sd's JM.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float vfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ f32x2 vfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ float vrcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ f32x2 vrcp(f32x2 x) { return f32x2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; }
+
+template <typename V>
+__device__ __forceinline__ V relax_dev(V f[9], const KBase<float>& b, const KForce<float>& k) {
+#pragma clang fp contract(off)
+    V s[4], d[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        s[p] = f[pair_a(p)] + f[pair_b(p)];
+        d[p] = f[pair_a(p)] - f[pair_b(p)];
+    }
+    const V sum = f[0] + ((s[0] + s[1]) + (s[2] + s[3]));
+    const V mx = d[0] + (d[2] - d[3]);
+    const V my = d[1] + (d[2] + d[3]);
+    const V rho = (V)1.f + sum;
+    V inv = vrcp(rho);  // + one Newton step (recip(float))
+    inv = vfma(inv, vfma(-rho, inv, (V)1.f), inv);
+    const V jx = mx + (V)k.hFx, jy = my + (V)k.hFy;
+    const V ux = jx * inv, uy = jy * inv;
+    const V usq = vfma(uy, uy, ux * ux);
+    const V uF = vfma(uy, (V)k.Fy, ux * (V)k.Fx);
+    const V base = -usq * (V)b.a1;
+    const V rb = vfma(rho, base, sum);
+    f[0] = vfma((V)b.omp, f[0], rb * (V)b.opw0);
+    V P[2], Qa[2];
+#pragma unroll
+    for (int cl = 0; cl < 2; ++cl) {
+        P[cl] = vfma(rb, (V)b.opw[cl], uF * (V)b.nck[cl]);
+        Qa[cl] = vfma(sum, (V)b.oqa[cl], (V)b.oqa[cl]);
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int cl = p < 2 ? 0 : 1;
+        const V cu = p == 0 ? ux : (p == 1 ? uy : (p == 2 ? ux + uy : uy - ux));
+        const V cj = p == 0 ? jx : (p == 1 ? jy : (p == 2 ? jx + jy : jy - jx));
+        const V E = vfma(cu, vfma(Qa[cl], cu, (V)k.hE[p]), P[cl]);
+        const V O = vfma((V)b.omwi2[cl], cj, (V)k.gO[p]);
+        const V A = vfma(s[p], (V)b.hs, E);
+        const V B = vfma(d[p], (V)b.hd, O);
+        f[pair_a(p)] = A + B;
+        f[pair_b(p)] = A - B;
+    }
+    return ux;
+}
+
 // One cell of a collide-stream step: f = the pulled populations f^t (deviations if DEV), k = the
 // constants of the cell's force (body force + IB force).  rho and u^t = (sum c f + F/2)/rho
 // (ImmersedBoundary.cu:249-255) from f, then collide in place; returns u_x (flux sample).
@@ -292,6 +347,7 @@ __device__ __forceinline__ float recip(float x) {
 template <typename R, bool DEV>
 __device__ __forceinline__ R relax_cell(R f[9], const KBase<R>& b, const KForce<R>& k) {
 #pragma clang fp contract(on)
+    if constexpr (DEV) return relax_dev<R>(f, b, k);
     R s[4], d[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {

@@ -37,7 +37,7 @@ namespace iblb {
 
 // sweep only (MODE bits 1, 2 as in lbm_vec.h): no software prefetch of the next column (two-step
 // sweeps); the deep sweep's wall split (sweepk_kernel)
-enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16 };
+enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16, MODE_PACK = 64 };
 
 namespace {
 
@@ -480,9 +480,31 @@ __device__ __forceinline__ void load_raw_periodic(const Sweep2Args<T>& a, int x,
     }
 }
 
+// f32, two cells per lane: both cells' collides as one packed f32x2 computation (relax_dev)
+template <typename T, int VS, int MODE>
+constexpr bool packed_pair() { return sizeof(T) == 4 && VS == 2 && (MODE & MODE_PACK); }
+template <typename T, int VS>
+__device__ __forceinline__ void relax_pair(const T (&s)[9][VS], const Sweep2Args<T>& a, bool flux, int fown, double& q,
+                                           T (&out)[9][VS]) {
+    f32x2 f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = f32x2{(float)s[k][0], (float)s[k][1]};
+    const f32x2 ux = relax_dev<f32x2>(f, kbase<float>(a.k), kbody<float>(a.k));
+    if (flux) {  // wave-uniform branch; the lane condition as a select (no exec-mask branch)
+        const double t0 = (double)ux.x / a.flux_norm, t1 = (double)ux.y / a.flux_norm;
+        q += (fown & 1) ? t0 : 0.;
+        q += (fown & 2) ? t1 : 0.;
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        out[k][0] = (T)f[k].x;
+        out[k][1] = (T)f[k].y;
+    }
+}
+
 // one column of level l+1 from a window of level l (A = older, B = middle, C = newer column in
 // walking direction DX): the output is B's column; flux: add u_x of the owned rows to q
-template <typename T, int VS, int DX>
+template <typename T, int VS, int DX, int MODE = 0>
 __device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (&B)[9][VS], const T (&C)[9][VS],
                                                   const Sweep2Args<T>& a, int lane, int r0, int et, bool walls,
                                                   bool flux, int fown, double& q, T (&out)[9][VS]) {
@@ -493,6 +515,10 @@ __device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (
     for (int k = 0; k < 9; ++k) pk[k] = cx(k) == DX ? &A[k] : (cx(k) == -DX ? &C[k] : &B[k]);
     T s[9][VS];
     pull_window<T, VS>(pk, nullptr, B[2], B[4], B[7][0], B[8][0], B[5], B[6], lane, r0, et, s, walls);
+    if constexpr (packed_pair<T, VS, MODE>()) {
+        relax_pair<T, VS>(s, a, flux, fown, q, out);
+        return;
+    }
 #pragma unroll
     for (int e = 0; e < VS; ++e) {
         R f[9];
@@ -509,7 +535,7 @@ __device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (
 }
 
 // level 1 of one column from its loaded g^t rows
-template <typename T, int VS>
+template <typename T, int VS, int MODE = 0>
 __device__ __forceinline__ void level_from_raw(const Raw<T, VS>& cur, const Sweep2Args<T>& a, int lane, int r0, int et,
                                                bool walls, bool flux, int fown, double& q, T (&out)[9][VS]) {
     typedef typename Calc<T>::R R;
@@ -522,6 +548,10 @@ __device__ __forceinline__ void level_from_raw(const Raw<T, VS>& cur, const Swee
 #pragma unroll
     for (int e = 0; e < VS; ++e) { t5[e] = cur.w[2]; t6[e] = cur.w[3]; }
     pull_window<T, VS>(pk, cur.e, cur.v[2], cur.v[4], cur.w[0], cur.w[1], t5, t6, lane, r0, et, s, walls);
+    if constexpr (packed_pair<T, VS, MODE>()) {
+        relax_pair<T, VS>(s, a, flux, fown, q, out);
+        return;
+    }
 #pragma unroll
     for (int e = 0; e < VS; ++e) {
         R f[9];
@@ -563,7 +593,7 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
     const int x = x0 + i * DX;
     T N[9][VS];
     // fin: the flux column is one of the sweep's outputs; level l reaches it at step fi + l - 1
-    level_from_raw<T, VS>(cur, a, lane, r0, et, walls, fin && i == fi, fown, q, N);
+    level_from_raw<T, VS, MODE>(cur, a, lane, r0, et, walls, fin && i == fi, fown, q, N);
     if (i + 1 < nl1) {
         // the resources of the next column triple: one new column
         if (DX > 0) {
@@ -583,7 +613,7 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
         const bool flux = fin && i == fi + l - 1;
         T out[9][VS];
         const bool made = i >= 2 * (l - 1);
-        if (made) level_from_window<T, VS, DX>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, fown, q, out);
+        if (made) level_from_window<T, VS, DX, MODE>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, fown, q, out);
         // level K's columns of the made steps are exactly the sweep's outputs [xa, xb)
         if (made && l == K && owner) {
             const __amdgpu_buffer_rsrc_t rd = col_rsrc<T>(a.dst + (long)c * a.L.col);
@@ -825,11 +855,17 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
         if ((a.variant & 2) && a.col_step <= 0 && top > OWN1) {
             b.wall_top = top;
             b.wall_ch0 = (top - OWN1 + rows_per_wave - 1) / rows_per_wave;
+            // bit 3: the inner chunks packed, two waves per SIMD (the packed inner walk needs 191 VGPRs;
+            // forced to three waves it spills 21 dwords: 0.417 vs 0.323 ms per M f32 launch, profiles/r04/pack)
+            if (a.variant & 8) return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PACK, K, SLAB, 2>(b, s, stop, start);
             if (a.variant & 1) return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT, K, SLAB, 3>(b, s, stop, start);
             return launch_sweepk_mode<T, VS, MODE_SPLIT, K, SLAB, 3>(b, s, stop, start);
         }
     }
-    // variants: bit 0 = nontemporal stores (default), 0 = plain
+    // variants: bit 0 = nontemporal stores (default), 0 = plain; bit 3 (f32, two cells per lane): the
+    // packed collide (both cells in one f32x2 computation, relax_dev)
+    if constexpr (sizeof(T) == 4 && VS == 2)
+        if (a.variant & 8) return launch_sweepk_mode<T, VS, 1 | MODE_PACK, K, SLAB, 1>(b, s, stop, start);
     if (a.variant & 1) return launch_sweepk_mode<T, VS, 1, K, SLAB, 1>(b, s, stop, start);
     return launch_sweepk_mode<T, VS, 0, K, SLAB, 1>(b, s, stop, start);
 }

@@ -6,4 +6,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 grep smoke $OUT/smoke.log
 timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-TAG=r04a WIDTHS=512 bash scripts/r03_scaling.sh
+TAG=r04a WIDTHS=512 bash scripts/archive/r03_scaling.sh

@@ -574,7 +574,8 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
     the chunk-edge ghost rows shrinking by one per level, ceil((K-1)/VS) ghost lanes per edge)
     equal one-step launches bit for bit, for every cells-per-lane width, sweep length (fixed
     and balanced to whole rounds of waves), variant (f32 variants 2, 3: the wall-row chunks as
-    their own sweep family of the three-wave build), wave order and walking direction, on
+    their own sweep family of the three-wave build; 8, 9, 11: the packed two-cell collide, 11 with
+    the wall chunks split off), wave order and walking direction, on
     ragged shapes including fewer columns than the K-column reach (periodic images wrap more
     than once).  1 + 10K + 2 steps = boot + 10 deep launches + one two-iteration launch."""
     from cuda_iblb_11_amd import workloads as W
@@ -591,7 +592,8 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
         monkeypatch.setenv("IBLB_SWEEP", "1")
         monkeypatch.setenv("IBLB_SWEEP_DEPTH", str(depth))
         for vs in vss:
-            for w, var, bal in [(4, 1, 0), (1, 0, 0), (3, 1, 1), (32, 1, 0), (7, 0, 1), (48, 1, 1), (5, 3, 1), (48, 2, 1)]:
+            for w, var, bal in [(4, 1, 0), (1, 0, 0), (3, 1, 1), (32, 1, 0), (7, 0, 1), (48, 1, 1), (5, 3, 1), (48, 2, 1),
+                                (5, 9, 1), (6, 8, 0), (48, 11, 1), (5, 11, 1)]:
                 monkeypatch.setenv("IBLB_DEEP_VS", str(vs))
                 monkeypatch.setenv("IBLB_DEEP_W", str(w))
                 monkeypatch.setenv("IBLB_DEEP_VARIANT", str(var))
