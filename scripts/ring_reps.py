@@ -1,10 +1,14 @@
 #!/usr/bin/env python3
 """Repeatability of the slab cycle inside ONE process: a slab (optionally the
 RCCL self ring, optionally with the K5 filament array) primed once, then REPS timed regions of
-STEPS iterations each; prints one JSON line with the ms/iteration of every repetition, the spread
-(max/min - 1) and the host time the submission of a region took before its synchronisation.
+STEPS iterations each; prints one JSON line with the ms/iteration of every repetition and the
+spread (max/min - 1).
 
-usage: scripts/ring_reps.py NX NY PRECISION [--ring] [--k5 OFFSET] [--reps 7] [--steps 300]
+usage: scripts/ring_reps.py NX NY PRECISION [--ring] [--k5 OFFSET] [--reps 7] [--steps 300] [--same-phase]
+
+--same-phase (with --k5): every timed region gets the points of the same STEPS iterations of the
+beat (the lattice state goes on), so the regions do the same work; without it the regions follow
+the beat, whose filament tilt (up to 8 columns) changes the band plans from region to region.
 """
 import argparse
 import json
@@ -27,6 +31,7 @@ def main():
     p.add_argument("--k5", type=float, default=None, help="K5 filaments (8 per 1024 columns) at this offset")
     p.add_argument("--reps", type=int, default=7)
     p.add_argument("--steps", type=int, default=300)
+    p.add_argument("--same-phase", action="store_true")
     a = p.parse_args()
     import cuda_iblb_11_amd as P
     from cuda_iblb_11_amd import workloads as W
@@ -44,10 +49,11 @@ def main():
         lat.attach_rccl(P.rccl_unique_id(), 1, 0)
     t = [0]
 
-    def stage(n):
+    def stage(n, t0=None):
         if pts is None:
             return
-        e = [pts(it) for it in range(t[0], t[0] + n)]
+        t0 = t[0] if t0 is None else t0
+        e = [pts(it) for it in range(t0, t0 + n)]
         lat.set_lagrangian_steps(np.stack([x[0] for x in e]), np.stack([x[1] for x in e]), np.stack([x[2] for x in e]))
 
     def run(n):
@@ -59,8 +65,9 @@ def main():
     while time.perf_counter() - t0 < 1.0:  # prime: the clock settles under load
         run(50)
     reps = []
+    phase0 = t[0]
     for _ in range(a.reps):
-        stage(a.steps)  # the points given ahead outside the timed region
+        stage(a.steps, phase0 if a.same_phase else None)  # the points given ahead outside the timed region
         lat.synchronize()
         ts = time.perf_counter()
         lat.step(a.steps)
@@ -69,6 +76,7 @@ def main():
         reps.append((time.perf_counter() - ts) / a.steps * 1e3)
     tm = lat.timing()
     print(json.dumps({"nx": a.nx, "ny": a.ny, "precision": a.precision, "ring": a.ring, "k5": a.k5,
+                      "same_phase": a.same_phase,
                       "ms_per_iter": [round(r, 5) for r in reps], "min": round(min(reps), 5),
                       "median": round(float(np.median(reps)), 5), "spread": round(max(reps) / min(reps) - 1, 4),
                       "band_cycles": tm["band_cycles"], "band_merged_cycles": tm["band_merged_cycles"]}), flush=True)
