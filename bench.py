@@ -430,7 +430,8 @@ def main():
                                "the rest in the deep sweep" if ns and tm["sweepk_launches"] else ""),
                 "nx": nx, "ny": ny, "global_cells": cells, "ib_points": ns,
                 **({"filament_offset": a.filament_offset} if wpts == "array" else {}),
-                **({"band_cycles": int(tm["band_cycles"]), "band_merged_cycles": int(tm["band_merged_cycles"])}
+                **({"band_cycles": int(tm["band_cycles"]), "band_merged_cycles": int(tm["band_merged_cycles"]),
+                    "band_par_cycles": int(tm["band_par_cycles"])}
                    if ns else {}),
                 "parallelism": f"x-slab x{world}" + (" (RCCL halo)" if world > 1 and not rehearsal else "")
                                + (" (RCCL self-ring rehearsal)" if a.rccl_self and world == 1 else "")

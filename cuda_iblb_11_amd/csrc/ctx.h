@@ -146,6 +146,11 @@ struct iblb_ctx {
     uint8_t* bfl_alloc = nullptr;  // ... and their chunk flags (zero between cycles)
     double* bfd[2] = {nullptr, nullptr};
     uint8_t* bfl[2] = {nullptr, nullptr};
+    int band_par_env = 1;        // IBLB_BAND_PAR: a lone slab's last level beside the deep sweep
+    bool band_par = false;       // the installed plan runs it (patch output rows skipped by the deep sweep)
+    bool band_prev_par = false;  // the last band cycle ran it (its deep sweep ended on ev_deep)
+    std::vector<iblb::SkipBox> band_skip;  // the plan's patch output regions (own columns, even rows)
+    hipEvent_t ev_deep = nullptr;  // the last band cycle's deep sweep done (PAR cycles)
     int band_reserve = 0;        // CUs of the band chain's stream (0: one stream, in sequence; -2: unmasked)
     bool band_sticky = false;    // keep the streams while a schedule runs
     hipStream_t band_st = nullptr;  // the band chain (masked to the reserved CUs)
@@ -188,7 +193,7 @@ struct iblb_ctx {
     double fused_ms = 0., ib_ms = 0., halo_ms = 0., sweep_ms = 0., sweepk_ms = 0.;
     long long fused_launches = 0, fused_cells = 0, sweep_launches = 0, sweep_cells = 0, sweepk_launches = 0,
               sweepk_cells = 0;
-    long long band_cycles = 0, band_merged_cycles = 0;  // IB band cycles run (counted without events too)
+    long long band_cycles = 0, band_merged_cycles = 0, band_par_cycles = 0;  // IB band cycles run (counted without events too)
     struct EvRec { int kind; size_t idx; long long cells; };
     std::vector<EvRec> ev_kind;
     std::string err;

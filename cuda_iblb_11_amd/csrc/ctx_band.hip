@@ -117,7 +117,7 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
         HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->deep_st, (uint32_t)deep.size(), deep.data()));
         HIP_TRY(c, hipExtStreamCreateWithCUMask(&c->band_st, (uint32_t)band.size(), band.data()));
     }
-    for (hipEvent_t* e : {&c->ev_b0, &c->ev_bd})
+    for (hipEvent_t* e : {&c->ev_b0, &c->ev_bd, &c->ev_deep})
         if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventDisableSystemFence));
     c->band_reserve = (int)want;
     return IBLB_OK;
@@ -216,9 +216,12 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     c->band_valid = false;
     // Rows: a patch's output rows [ya, yb) = its forced rows +- (K-1); level j covers K-1-j more on
     // each side (the deep sweep advances every row, the last level overwrites the output rows)
+    // (even bounds: a lane of the deep sweep's two-cell walk is then wholly in or out of a patch
+    // output, which the deep sweep leaves to the last level when the two run side by side)
     const int V64 = 64 * c->V;  // rows per chunk of the one-step kernel
     std::vector<std::array<int, 2>> pr(b.size());
-    for (size_t q = 0; q < b.size(); ++q) pr[q] = {std::max(0, b[q][2] - (K - 1)), std::min(ny, b[q][3] + K)};
+    for (size_t q = 0; q < b.size(); ++q)
+        pr[q] = {std::max(0, b[q][2] - (K - 1)) & ~1, std::min(ny, (b[q][3] + K + 1) & ~1)};
     std::vector<int> tab;
     std::vector<int> off((size_t)K), cnt((size_t)K), nchl((size_t)K, 0);
     long long band_lu = 0;
@@ -315,6 +318,27 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     c->band_b = b;
     c->band_d = bd;
     c->band_x = bx;
+    // PAR (two streams): the last level beside the deep sweep (and a group slab's boundary sweeps),
+    // which skip the patch outputs — the last level's entries: own columns [x0 - (K-1), x1 + (K-1)],
+    // rows pr.  Only where those regions stay disjoint in columns (periodic images of a tiny slab
+    // could overlap) and fit the kernel arguments.
+    // IBLB_BAND_PAR 1 (auto): where the chain, not the deep sweep, is the cycle's critical path (the
+    // merged chain's criterion: narrow slabs) — the deep sweep's per-column skip test costs it 9-14 %
+    // (K3 114k vs 118k, K5 193k vs 218k MLUPS with it, profiles/r04/par); 2: always; 0: never
+    c->band_skip.clear();
+    c->band_par = false;
+    const double deep_us = (double)K * deep_cols * ny / (is_f64(c) ? 130e3 : 190e3);
+    if (c->band_st && (c->band_par_env == 2 || (c->band_par_env == 1 && deep_us < 1.5 * 2 * K * 8.0))) {
+        bool ok = b.size() <= (size_t)MAX_SKIP;
+        for (size_t q = 0; ok && q < b.size(); ++q) {
+            const int x0 = std::max(0, b[q][0] - (K - 1)), x1 = std::min(ncol - 1, b[q][1] + (K - 1));
+            if (x0 > x1) continue;
+            if (!c->band_skip.empty() && x0 <= c->band_skip.back().x1) ok = false;
+            c->band_skip.push_back(SkipBox{x0, x1, pr[q][0], pr[q][1]});
+        }
+        c->band_par = ok && !c->band_skip.empty();
+        if (!c->band_par) c->band_skip.clear();
+    }
     c->band_valid = true;
     return IBLB_OK;
 }
@@ -366,10 +390,14 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
         d.fskip0 = c->band_fy0;
         d.fskip1 = c->band_fy1;
     }
+    if (c->band_par) {  // the patch outputs are the last level's (it runs beside, on the chain's stream)
+        d.nskip = (int)c->band_skip.size();
+        std::copy(c->band_skip.begin(), c->band_skip.end(), d.skip);
+    }
     size_t ev = 0;
     int rc = ev_begin(c, &ev, ds);
     if (rc) return rc;
-    HIP_TRY(c, launch_sweepk<T>(d, K, false, ds));
+    HIP_TRY(c, launch_sweepk<T>(d, K, false, ds, c->band_par ? c->ev_deep : nullptr));
     return ev_end(c, ev, EV_SWEEPK, (long long)n * c->ny, ds);
 }
 
@@ -497,7 +525,7 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
             }
         }
         hipStream_t ls = bs;
-        if (j == K - 1) {
+        if (j == K - 1 && !c->band_par) {
             if (bs != ds) {  // behind the deep sweep, on its stream
                 HIP_TRY(c, hipEventRecord(c->ev_bd, bs));
                 HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_bd, 0));
@@ -505,6 +533,8 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
             }
             if (slab && D > 0) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_bnd, 0));
             if (a.ncols <= 0 && a.clr_waves <= 0) HIP_TRY(c, hipEventRecord(c->band_end, ls));
+        } else if (j == K - 1 && a.ncols <= 0 && a.clr_waves <= 0) {  // PAR: right after the chain
+            HIP_TRY(c, hipEventRecord(c->band_end, ls));
         }
         if (a.ncols <= 0 && a.nns <= 0 && a.clr_waves <= 0) continue;
         size_t ev = 0;
@@ -546,6 +576,16 @@ static int band_step(iblb_ctx* c) {
             HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_b0, 0));
             HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_b0, 0));
         }
+    } else if (c->band_prev_par) {
+        // the last cycle's deep sweep (ds) and last level (bs) wrote disjoint parts of g^t; each stream
+        // waits for the other's: the chain reads g^t, the deep sweep reads it and overwrites the
+        // buffer the last cycle's chain read
+        HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_deep, 0));
+        HIP_TRY(c, hipStreamWaitEvent(ds, c->band_end, 0));
+        if (slab) {  // boundary(t-K) wrote columns both read
+            HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_bnd, 0));
+            HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_bnd, 0));
+        }
     } else {
         HIP_TRY(c, hipStreamWaitEvent(bs, c->band_end, 0));  // g^t complete: the last level of t-K on ds
         if (slab) {  // boundary(t-K) wrote columns both read
@@ -556,18 +596,28 @@ static int band_step(iblb_ctx* c) {
     if (slab) {
         // everything before this cycle, seen from the comm stream: the previous cycle's end on ds
         // (chained) or the context's stream
+        // (a PAR cycle ends on two streams: its last level on bs, its deep sweep on ds)
         hipEvent_t before = chained ? c->band_end : c->ev_pre;
+        const bool before_deep = chained && c->band_prev_par;
         hipStream_t cs = c->comm_stream;
-        if (c->band_x > c->bnd_w) HIP_TRY(c, hipStreamWaitEvent(cs, before, 0));
+        if (c->band_x > c->bnd_w) {
+            HIP_TRY(c, hipStreamWaitEvent(cs, before, 0));
+            if (before_deep) HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_deep, 0));
+        }
         if ((rc = exchange(c, cs, c->band_x))) return rc;
         if (D > 0) HIP_TRY(c, hipEventRecord(c->ev_x, cs));
         HIP_TRY(c, hipStreamWaitEvent(cs, before, 0));
+        if (before_deep) HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_deep, 0));
         Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
         b.vs = c->slab_vs;
         b.variant = c->deep_variant;
         if (c->band_flux >= 0) {
             b.fskip0 = c->band_fy0;
             b.fskip1 = c->band_fy1;
+        }
+        if (c->band_par) {  // the patch outputs of the edge columns are the last level's
+            b.nskip = (int)c->band_skip.size();
+            std::copy(c->band_skip.begin(), c->band_skip.end(), b.skip);
         }
         HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));
@@ -582,8 +632,10 @@ static int band_step(iblb_ctx* c) {
     // level and the next deep sweep left ~7 us of idle queue per cycle, profiles/r03ch2)
     c->band_end = c->band_pin_ev[c->band_pin_cur];  // (the waits above took the previous cycle's)
     if ((rc = band_chain<T>(c, K, A, B, S, slab, bs, ds))) return rc;
+    c->band_prev_par = c->band_par;
     c->band_cycles++;
     if (c->band_merged && c->bf_alloc) c->band_merged_cycles++;
+    if (c->band_par) c->band_par_cycles++;
     c->band_run = ov;
     if (slab) {
         c->bnd_w = D > 0 ? 0 : K;  // the edge columns of g^{t+K}: the boundary sweeps' unless a trapezoid stored them
@@ -602,8 +654,10 @@ static int band_step(iblb_ctx* c) {
 int band_join(iblb_ctx* c) {
     if (!c->band_run) return IBLB_OK;
     c->band_run = false;
-    // band_end follows the whole cycle: ds waited for the chain (ev_bd) before its last level
+    // band_end follows the whole cycle: ds waited for the chain (ev_bd) before its last level;
+    // a PAR cycle ends on both streams (last level on bs, deep sweep on ds)
     HIP_TRY(c, hipStreamWaitEvent(c->stream, c->band_end, 0));
+    if (c->band_prev_par) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_deep, 0));
     if (rccl_multi(c)) HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));  // comm_ready's "last step"
     return IBLB_OK;
 }
@@ -617,9 +671,11 @@ int band_release(iblb_ctx* c) {
             (void)hipStreamDestroy(st);
         }
     c->band_st = c->deep_st = nullptr;
-    for (hipEvent_t e : {c->ev_b0, c->ev_bd})
+    for (hipEvent_t e : {c->ev_b0, c->ev_bd, c->ev_deep})
         if (e) (void)hipEventDestroy(e);
-    c->ev_b0 = c->ev_bd = nullptr;
+    c->ev_b0 = c->ev_bd = c->ev_deep = nullptr;
+    c->band_par = c->band_prev_par = false;
+    c->band_skip.clear();
     c->band_end = nullptr;
     c->band_run = false;
     c->band_pin_cur = -1;

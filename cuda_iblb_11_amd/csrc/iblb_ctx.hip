@@ -343,6 +343,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_merge = (int)env_long("IBLB_BAND_MERGE", 1);
+    c->band_par_env = (int)env_long("IBLB_BAND_PAR", 1);
     // one cell per lane in a group slab's deep sweeps (self ring 512 / 1024 / 2048 x 4096: 0.0347 /
     // 0.0542 / 0.0935 ms/iteration vs 0.0380 / 0.0568 / 0.0942 with two, profiles/r01e7_*)
     c->slab_vs = 1;
@@ -759,8 +760,9 @@ int iblb_get_timing(iblb_ctx* c, iblb_timing* t, int reset) {
     t->sweepk_depth = c->sweep_depth;
     t->band_cycles = c->band_cycles;
     t->band_merged_cycles = c->band_merged_cycles;
+    t->band_par_cycles = c->band_par_cycles;
     if (reset) {
-        c->band_cycles = c->band_merged_cycles = 0;
+        c->band_cycles = c->band_merged_cycles = c->band_par_cycles = 0;
         c->fused_ms = c->ib_ms = c->halo_ms = c->sweep_ms = c->sweepk_ms = 0.;
         c->fused_launches = c->fused_cells = c->sweep_launches = c->sweep_cells = 0;
         c->sweepk_launches = c->sweepk_cells = 0;

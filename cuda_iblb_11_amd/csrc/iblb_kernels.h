@@ -72,6 +72,14 @@ struct FusedArgs {
 };
 
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.
+// IB band cycle with its last level beside the deep sweep (lone slab): a patch output region the
+// last level stores and the deep sweep must not: local columns [x0, x1] (inclusive) x rows [y0, y1)
+// (even bounds, so that a lane's two cells are both in or both out)
+struct SkipBox {
+    int x0, x1, y0, y1;
+};
+constexpr int MAX_SKIP = 96;
+
 template <typename T>
 struct Sweep2Args {
     const T* src;        // g^t
@@ -96,6 +104,8 @@ struct Sweep2Args {
     double* Q;
     Coef c;
     KConst k;            // collide constants folded on the host (iblb_device.h)
+    int nskip = 0;       // > 0: the patch output regions below are left to the band's last level,
+    SkipBox skip[MAX_SKIP];  // sorted by x0, disjoint in columns (lone slab only)
 };
 
 // ghost: false = lone slab (columns outside [0, ncol) are the periodic images; also the interior

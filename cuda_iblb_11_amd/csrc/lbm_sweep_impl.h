@@ -31,13 +31,15 @@
 
 #include <hip/hip_ext.h>
 
+#include <climits>
+
 #include "lbm_vec.h"
 
 namespace iblb {
 
 // sweep only (MODE bits 1, 2 as in lbm_vec.h): no software prefetch of the next column (two-step
 // sweeps); the deep sweep's wall split (sweepk_kernel)
-enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16, MODE_PACK = 64 };
+enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16, MODE_PACK = 64, MODE_SKIP = 128 };
 
 namespace {
 
@@ -575,6 +577,43 @@ __device__ __forceinline__ void copy_col(T (&d)[9][VS], const T (&s)[9][VS]) {
         for (int e = 0; e < VS; ++e) d[k][e] = s[k][e];
 }
 
+// MODE_SKIP: the patch output regions (left to the band cycle's last level) a walk meets.  The walk's
+// output columns are monotonic, so the wave keeps the region it is at or before: its index sp, its
+// columns in scalar registers and whether this lane's rows r0 .. r0+VS-1 lie in its rows; it moves
+// on (reading the next region from the kernel arguments) only when the walk passes the region.
+struct SkipState {
+    int sp, x0, x1;
+    bool rows;
+};
+template <typename T, int VS, bool REV>
+__device__ __forceinline__ void skip_load(const Sweep2Args<T>& a, int r0, SkipState& st) {
+    if (st.sp >= 0 && st.sp < a.nskip) {
+        const SkipBox b = a.skip[st.sp];
+        st.x0 = b.x0;
+        st.x1 = b.x1;
+        st.rows = r0 >= b.y0 && r0 + VS <= b.y1;
+    } else {  // no region left on this side: a column range no output column reaches
+        st.x0 = INT_MAX;
+        st.x1 = INT_MIN;
+        st.rows = false;
+    }
+}
+template <typename T, int VS, bool REV>
+__device__ __forceinline__ bool skip_rows(const Sweep2Args<T>& a, int c, int r0, SkipState& st) {
+    if (!REV) {
+        while (st.sp < a.nskip && c > st.x1) {
+            ++st.sp;
+            skip_load<T, VS, REV>(a, r0, st);
+        }
+    } else {
+        while (st.sp >= 0 && c < st.x0) {
+            --st.sp;
+            skip_load<T, VS, REV>(a, r0, st);
+        }
+    }
+    return c >= st.x0 && c <= st.x1 && st.rows;
+}
+
 // Iteration i of the walk (column x = x0 + i*dx): level 1 of x from the rows loaded in the
 // previous iteration, then the loads of column x + dx (they fly during the remaining levels),
 // then level l = 2 .. K of column x - (l-1)*dx from level l-1's window: WA / WB = its columns
@@ -588,7 +627,7 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
                                             unsigned off, int lane, int r0, int et, bool owner, bool bot, bool top,
                                             bool walls, T (&WA)[K - 1][9][VS], T (&WB)[K - 1][9][VS],
                                             Raw<T, VS>& cur, double& q, const BufOfs& bo,
-                                            __amdgpu_buffer_rsrc_t (&rc)[3], bool fin, int fi, int fown) {
+                                            __amdgpu_buffer_rsrc_t (&rc)[3], bool fin, int fi, int fown, SkipState& sp) {
     constexpr int DX = REV ? -1 : 1;
     const int x = x0 + i * DX;
     T N[9][VS];
@@ -615,7 +654,10 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
         const bool made = i >= 2 * (l - 1);
         if (made) level_from_window<T, VS, DX, MODE>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, fown, q, out);
         // level K's columns of the made steps are exactly the sweep's outputs [xa, xb)
-        if (made && l == K && owner) {
+        bool keep = owner;
+        if constexpr ((MODE & MODE_SKIP) != 0)
+            if (made && l == K) keep = owner && !skip_rows<T, VS, REV>(a, c, r0, sp);
+        if (made && l == K && keep) {
             const __amdgpu_buffer_rsrc_t rd = col_rsrc<T>(a.dst + (long)c * a.L.col);
 #pragma unroll
             for (int k = 0; k < 9; ++k) st_rows_buf<T, VS, MODE>(rd, bo.lane, (unsigned)k * bo.plane, out[k]);
@@ -665,9 +707,18 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
     for (int e = 0; e < VS; ++e) fown |= (owner && flux_row(a, r0 + e)) ? 1 << e : 0;
     // (a main loop without the per-level `made` checks, after 2(K-1) window-filling iterations,
     // lets the compiler hoist the collide constants into registers: VGPR spills, 512 VGPRs)
+    SkipState sp{0, INT_MAX, INT_MIN, false};  // MODE_SKIP: the first region not left of the sweep (REV: right)
+    if constexpr ((MODE & MODE_SKIP) != 0) {
+        if (!REV)
+            while (sp.sp < a.nskip && a.skip[sp.sp].x1 < xa) ++sp.sp;
+        else
+            for (sp.sp = a.nskip - 1; sp.sp >= 0 && a.skip[sp.sp].x0 >= xb; --sp.sp) {
+            }
+        skip_load<T, VS, REV>(a, r0, sp);
+    }
     for (int i = 0; i < nl1; ++i)
         sweepk_iter<T, VS, MODE, K, SLAB, REV>(a, i, nl1, x0, xa, xb, row0, off, lane, r0, et, owner, bot, top, walls, WA,
-                                               WB, cur, q, bo, rc, fin, fi, fown);
+                                               WB, cur, q, bo, rc, fin, fi, fown, sp);
     return q;
 }
 
@@ -862,6 +913,8 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
             return launch_sweepk_mode<T, VS, MODE_SPLIT, K, SLAB, 3>(b, s, stop, start);
         }
     }
+    // the IB band cycle's deep and boundary sweeps beside its last level: patch output rows left out
+    if (a.nskip > 0) return launch_sweepk_mode<T, VS, 1 | MODE_SKIP, K, SLAB, 1>(b, s, stop, start);
     // variants: bit 0 = nontemporal stores (default), 0 = plain; bit 3 (f32, two cells per lane): the
     // packed collide (both cells in one f32x2 computation, relax_dev)
     if constexpr (sizeof(T) == 4 && VS == 2)

@@ -150,6 +150,7 @@ typedef struct iblb_timing {
      * whether or not profiling events are on */
     long long band_cycles;
     long long band_merged_cycles;
+    long long band_par_cycles;  /* of those, run with the last level beside the deep sweep (lone slab) */
 } iblb_timing;
 
 /* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */

@@ -386,3 +386,27 @@ def test_moving_points_across_x0(gpu, oracle, precision, monkeypatch):
     r = fields(lat, sim)
     assert max(r["rho-1"], r["ux"], r["uy"]) <= (1e-10 if precision == "f64" else TOL32), r
     assert abs(lat.flux - sim.flux) <= (1e-9 if precision == "f64" else 1e-4) * max(abs(sim.flux), 1e-30)
+
+
+@pytest.mark.parametrize("precision,merge", [("f64", "1"), ("f32", "1"), ("f64", "0")])
+def test_ib_band_par_equals_serial(gpu, oracle, precision, merge, monkeypatch):
+    """The lone slab's band cycle with its last level beside the deep sweep (IBLB_BAND_PAR=2: the
+    deep sweep leaves the patch output rows to it) against the last level behind the deep sweep (0): filaments swaying across x = 0 (ghost trapezoids with periodic images) and next
+    to XDIM-1, moving every iteration (a new plan every cycle), readers between chunks; both against
+    the oracle and against each other up to the spread atomics' order."""
+    monkeypatch.setenv("IBLB_BAND_MERGE", merge)
+    nx, ny = 256, 128
+    out = {}
+    for par in ("2", "0"):  # always / never (the default, 1, picks it where the deep sweep is short)
+        monkeypatch.setenv("IBLB_BAND_PAR", par)
+        lat, sim = moving_run(gpu, oracle, nx, ny, _crossing(nx), [1, 12, 5, 3, 15], precision=precision,
+                              monkeypatch=monkeypatch, readers=True)
+        tm = lat.timing()
+        assert tm["band_cycles"] >= 6 and (tm["band_par_cycles"] == tm["band_cycles"]) == (par == "2"), tm
+        r = fields(lat, sim)
+        assert max(r["rho-1"], r["ux"], r["uy"]) <= (1e-10 if precision == "f64" else TOL32), (par, r)
+        out[par] = lat.macro()
+        lat.close()
+    (r1, u1), (r0, u0) = out["2"], out["0"]
+    tol = 1e-12 if precision == "f64" else 1e-5
+    assert rel(r1, r0) <= tol and rel(u1, u0) <= tol
