@@ -302,7 +302,10 @@ def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap, bulk, depth
     ib = {False: "0", True: "1"}.get(with_ib, with_ib)  # "2": interior filaments, band cycle
     cmd = [sys.executable, os.path.join(here, "mock_rccl", "run_group.py"), str(n), str(nx), "130", "25", ib,
            precision, str(bulk)]
-    env = dict(os.environ, IBLB_OVERLAP=str(overlap), IBLB_SWEEP_DEPTH=str(depth))
+    # ranks as threads: each rank's four streams would share HIP's default four hardware queues, so that
+    # one rank's cross-stream wait could block another rank's work queued behind it (a hang seen once in
+    # round 4); 16 queues keep the ranks' streams apart (the box refuses more than 32)
+    env = dict(os.environ, IBLB_OVERLAP=str(overlap), IBLB_SWEEP_DEPTH=str(depth), GPU_MAX_HW_QUEUES="16")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert lines, p.stdout + p.stderr
@@ -348,7 +351,7 @@ def test_full_size_decomposed(gpu, n, workload, merge):
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ)
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")  # (ranks as threads: see test_rccl_slab_path_threads)
     env.pop("IBLB_BAND_MERGE", None)
     if merge is not None:
         env["IBLB_BAND_MERGE"] = merge
