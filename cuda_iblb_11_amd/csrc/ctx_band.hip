@@ -381,10 +381,11 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     const int W = std::max(1, c->deep_w);
     Sweep2Args<T> d = sweep_args<T>(c, lo, c->deep_balance ? 0 : W, hi, (n + W - 1) / W, W);
     d.vs = slab ? c->slab_vs : c->deep_vs;
-    // the two-wave scalar-collide build: the three-wave f32 wall split leaves the chain's kernels no
-    // room beside the deep sweep (K5 197.6k vs 193.9k MLUPS with it, profiles/r03sp), and the packed
-    // builds (two waves of 191 / 228 VGPRs) measured 209k / 202k vs 215k (profiles/r04/pack)
-    d.variant = c->deep_variant & 1;
+    // f32: the two-wave scalar-collide build: the three-wave f32 wall split leaves the chain's kernels
+    // no room beside the deep sweep (K5 197.6k vs 193.9k MLUPS with it, profiles/r03sp), and the
+    // packed builds (two waves of 191 / 228 VGPRs) measured 209k / 202k vs 215k (profiles/r04/pack).
+    // f64: the configured variant (its wall split keeps one wave per SIMD; not with PAR's skip boxes)
+    d.variant = sizeof(T) == 8 ? c->deep_variant : c->deep_variant & 1;
     d.cus = c->ncu ? (slab ? c->ncu - c->reserved_cus : c->ncu) - std::max(0, c->band_reserve) : 0;
     if (c->band_flux >= 0) {
         d.fskip0 = c->band_fy0;

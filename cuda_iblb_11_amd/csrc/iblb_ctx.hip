@@ -337,16 +337,19 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->sweep_depth = (int)std::min(6L, std::max(2L, env_long("IBLB_SWEEP_DEPTH", 5)));
     c->deep_w = (int)env_long("IBLB_DEEP_W", f64 ? 96 : 64);
     c->deep_vs = (int)env_long("IBLB_DEEP_VS", 2);
-    // f32: the wall split (variant bit 1, three waves per SIMD: M f32 0.318 vs 0.341 ms per launch,
-    // profiles/r03sp)
-    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 1 : 11);
+    // f32: the wall split (variant bit 1) with the packed collide (bit 3), profiles/r04/pack; f64: the
+    // wall split with the level-1 preshift (bits 1, 5: M f64 0.480 vs 0.521 ms per launch,
+    // profiles/r04/split64)
+    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 35 : 11);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_merge = (int)env_long("IBLB_BAND_MERGE", 1);
     c->band_par_env = (int)env_long("IBLB_BAND_PAR", 1);
-    // one cell per lane in a group slab's deep sweeps (self ring 512 / 1024 / 2048 x 4096: 0.0347 /
-    // 0.0542 / 0.0935 ms/iteration vs 0.0380 / 0.0568 / 0.0942 with two, profiles/r01e7_*)
-    c->slab_vs = 1;
+    // cells per lane in a group slab's deep sweeps: f64 two (the wall split needs them: self ring
+    // 512 / 1024 / 2048 x 4096 0.0170 / 0.0293 / 0.0531 ms/iteration vs 0.0194 / 0.0343 / 0.0638
+    // with one, profiles/r04/split64); f32 one (1024 / 2048 x 2048: 0.0126 / 0.0203 vs 0.0133 /
+    // 0.0220 with two; round 1: profiles/r01e7_*)
+    c->slab_vs = env_long("IBLB_SLAB_VS", f64 ? 2 : 1) == 2 ? 2 : 1;
     // ghost columns: K for a deep cycle's halo, 3 for a one-step IB halo, 3K for the IB band
     // trapezoids that cross a slab edge (ctx_band.hip)
     c->gc = std::max(3, 3 * c->sweep_depth);

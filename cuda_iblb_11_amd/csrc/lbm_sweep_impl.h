@@ -39,7 +39,7 @@ namespace iblb {
 
 // sweep only (MODE bits 1, 2 as in lbm_vec.h): no software prefetch of the next column (two-step
 // sweeps); the deep sweep's wall split (sweepk_kernel)
-enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16, MODE_PACK = 64, MODE_SKIP = 128 };
+enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16, MODE_PACK = 64, MODE_SKIP = 128, MODE_PRESHIFT = 256 };
 
 namespace {
 
@@ -124,7 +124,8 @@ template <typename T, int VS>
 struct Raw {
     T v[9][VS];
     T e[9];  // wave-edge rows: row0-1 of the c_y = +1 planes, row0+64*VS of the c_y = -1 planes
-    T w[4];  // g0(x, 0, 7), g0(x, 0, 8), g0(x, Y-1, 5), g0(x, Y-1, 6) (wall lanes only)
+    T w[6];  // g0(x, 0, 7), g0(x, 0, 8), g0(x, Y-1, 5), g0(x, Y-1, 6) (wall lanes only); MODE_PRESHIFT:
+             // g0(x, 0, 4), g0(x, Y-1, 2)
 };
 
 // rows of the wave start at row0 = cs - VS (uniform); lane byte offset off
@@ -467,18 +468,26 @@ __device__ __forceinline__ void load_raw_periodic(const Sweep2Args<T>& a, int x,
     for (int k = 0; k < 9; ++k) {
         const __amdgpu_buffer_rsrc_t rk = rc[1 - cx(k)];
         const unsigned so = (unsigned)k * bo.plane;
-        ld_rows_buf<T, VS, MODE>(rk, bo.lane, so, r.v[k]);
-        if (cy(k) == 1) r.e[k] = ld_one_buf<T>(rk, bo.lo, so);
-        if (cy(k) == -1) r.e[k] = ld_one_buf<T>(rk, bo.hi, so);
+        if (MODE & MODE_PRESHIFT) {
+            // the lane's rows of the pull itself: rows r0 - c_y .. (one row off the lane's alignment; no
+            // wave-edge value and no lane shift at level 1)
+            ld_rows_buf<T, VS, MODE>(rk, bo.lane, so - cy(k) * (int)sizeof(T), r.v[k]);
+        } else {
+            ld_rows_buf<T, VS, MODE>(rk, bo.lane, so, r.v[k]);
+            if (cy(k) == 1) r.e[k] = ld_one_buf<T>(rk, bo.lo, so);
+            if (cy(k) == -1) r.e[k] = ld_one_buf<T>(rk, bo.hi, so);
+        }
     }
-    r.w[0] = r.w[1] = r.w[2] = r.w[3] = (T)0;
+    r.w[0] = r.w[1] = r.w[2] = r.w[3] = r.w[4] = r.w[5] = (T)0;
     if (bot) {
         r.w[0] = col_deep<T, SLAB, K>(a, x, 7)[0];
         r.w[1] = col_deep<T, SLAB, K>(a, x, 8)[0];
+        if (MODE & MODE_PRESHIFT) r.w[4] = col_deep<T, SLAB, K>(a, x, 4)[0];
     }
     if (top) {
         r.w[2] = col_deep<T, SLAB, K>(a, x, 5)[a.L.ny - 1];
         r.w[3] = col_deep<T, SLAB, K>(a, x, 6)[a.L.ny - 1];
+        if (MODE & MODE_PRESHIFT) r.w[5] = col_deep<T, SLAB, K>(a, x, 2)[a.L.ny - 1];
     }
 }
 
@@ -549,7 +558,29 @@ __device__ __forceinline__ void level_from_raw(const Raw<T, VS>& cur, const Swee
     T t5[VS], t6[VS];
 #pragma unroll
     for (int e = 0; e < VS; ++e) { t5[e] = cur.w[2]; t6[e] = cur.w[3]; }
-    pull_window<T, VS>(pk, cur.e, cur.v[2], cur.v[4], cur.w[0], cur.w[1], t5, t6, lane, r0, et, s, walls);
+    if (MODE & MODE_PRESHIFT) {  // loaded at the pull's rows; the walls' same-cell values are uniform loads
+        T m2[VS], m4[VS];
+#pragma unroll
+        for (int e = 0; e < VS; ++e) { m2[e] = cur.w[5]; m4[e] = cur.w[4]; }
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+#pragma unroll
+            for (int e = 0; e < VS; ++e) s[k][e] = cur.v[k][e];
+        if (walls) {
+            if (r0 == 0) {  // bounce-back on y = 0 (LatticeBoltzmann.cu:328-340)
+                s[2][0] = m4[0];
+                s[5][0] = cur.w[0];
+                s[6][0] = cur.w[1];
+            }
+            if (et >= 0 && et < VS) {  // same-cell mirror on y = Y-1 (LatticeBoltzmann.cu:341-353)
+#pragma unroll
+                for (int e = 0; e < VS; ++e)
+                    if (e == et) { s[4][e] = m2[e]; s[8][e] = t5[e]; s[7][e] = t6[e]; }
+            }
+        }
+    } else {
+        pull_window<T, VS>(pk, cur.e, cur.v[2], cur.v[4], cur.w[0], cur.w[1], t5, t6, lane, r0, et, s, walls);
+    }
     if constexpr (packed_pair<T, VS, MODE>()) {
         relax_pair<T, VS>(s, a, flux, fown, q, out);
         return;
@@ -888,9 +919,10 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
     return hipGetLastError();
 }
 
-// the f32 wall split (variant bit 1): two cells per lane, three waves per SIMD
+// the wall split (variant bit 1): two cells per lane in the inner chunks; f32 at three waves per
+// SIMD, f64 at one
 template <typename T, int VS>
-constexpr bool wall_split_built() { return sizeof(T) == 4 && VS == 2; }
+constexpr bool wall_split_built() { return VS == 2; }
 
 template <typename T, int VS, int K, bool SLAB>
 static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEvent_t stop, hipEvent_t start) {
@@ -903,14 +935,19 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
         // row (two-cell lanes of the inner chunks never straddle it) holding the last OWN1 or fewer rows
         constexpr int OWN1 = 64 - 2 * ghost_lanes<K, 1>();
         const int top = (a.L.ny - OWN1 + 1) & ~1;
-        if ((a.variant & 2) && a.col_step <= 0 && top > OWN1) {
+        if ((a.variant & 2) && a.col_step <= 0 && a.nskip == 0 && top > OWN1) {
             b.wall_top = top;
             b.wall_ch0 = (top - OWN1 + rows_per_wave - 1) / rows_per_wave;
             // bit 3: the inner chunks packed, two waves per SIMD (the packed inner walk needs 191 VGPRs;
             // forced to three waves it spills 21 dwords: 0.417 vs 0.323 ms per M f32 launch, profiles/r04/pack)
-            if (a.variant & 8) return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PACK, K, SLAB, 2>(b, s, stop, start);
-            if (a.variant & 1) return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT, K, SLAB, 3>(b, s, stop, start);
-            return launch_sweepk_mode<T, VS, MODE_SPLIT, K, SLAB, 3>(b, s, stop, start);
+            constexpr int WPE = sizeof(T) == 4 ? 3 : 1;
+            if constexpr (sizeof(T) == 4)
+                if (a.variant & 8)
+                    return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PACK, K, SLAB, 2>(b, s, stop, start);
+            if (a.variant & 32)
+                return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PRESHIFT, K, SLAB, WPE>(b, s, stop, start);
+            if (a.variant & 1) return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT, K, SLAB, WPE>(b, s, stop, start);
+            return launch_sweepk_mode<T, VS, MODE_SPLIT, K, SLAB, WPE>(b, s, stop, start);
         }
     }
     // the IB band cycle's deep and boundary sweeps beside its last level: patch output rows left out
@@ -919,6 +956,11 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
     // packed collide (both cells in one f32x2 computation, relax_dev)
     if constexpr (sizeof(T) == 4 && VS == 2)
         if (a.variant & 8) return launch_sweepk_mode<T, VS, 1 | MODE_PACK, K, SLAB, 1>(b, s, stop, start);
+    // bit 5 without bit 1: level 1 loads each plane at its pull's rows (no wave-edge loads, no lane
+    // shift) in every chunk.  Slower than the plain walk (M f64 0.559 vs 0.521 ms per launch,
+    // profiles/r04/split64): the wall waves, which set the launch time here, wait on the wall rows'
+    // uniform loads.  With bit 1 (the split) the inner chunks take it and the wall waves have slack.
+    if ((a.variant & 34) == 32) return launch_sweepk_mode<T, VS, 1 | MODE_PRESHIFT, K, SLAB, 1>(b, s, stop, start);
     if (a.variant & 1) return launch_sweepk_mode<T, VS, 1, K, SLAB, 1>(b, s, stop, start);
     return launch_sweepk_mode<T, VS, 0, K, SLAB, 1>(b, s, stop, start);
 }
