@@ -313,6 +313,14 @@ def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap, bulk, depth
     assert p.returncode == 0 and res["ok"], (res, p.stderr[-2000:])
 
 
+@pytest.mark.parametrize("n,precision,vs", [(3, "f64", "1"), (2, "f32", "2"), (4, "f32", "2")])
+def test_rccl_slab_cells_per_lane(gpu, n, precision, vs, monkeypatch):
+    """The slab deep sweeps with the other cells-per-lane width (IBLB_SLAB_VS; defaults: f64 two
+    cells with the wall split, f32 one): still bit-identical to one slab."""
+    monkeypatch.setenv("IBLB_SLAB_VS", vs)
+    test_rccl_slab_path_threads(gpu, n, False, precision, 1, 1, 5)
+
+
 @pytest.mark.parametrize("n,precision,mode", [(2, "f64", "2"), (3, "f32", "2"), (4, "f64", "2"), (2, "f64", "3"),
                                               (4, "f32", "3"), (5, "f64", "3"), (8, "f32", "3")])
 def test_rccl_slab_band_cycle_threads(gpu, n, precision, mode):
