@@ -891,7 +891,7 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
         long ns = (n + b.W - 1) / b.W;
         if (MODE & MODE_SPLIT) {
             // wall split: nin inner chunks with ns sweeps, the two wall chunks with ns * r sweeps each
-            const long nin = b.wall_ch0, r4 = WALL_SWEEPS_X4;
+            const long nin = b.wall_ch0, r4 = VS == 1 ? 6 : WALL_SWEEPS_X4;  // VS 1: wall walks ~1.4x the inner
             if (slots > 0) {
                 const long rounds = std::max(1L, (ns * (4 * nin + 2 * r4) / 4 + slots / 2) / slots);
                 ns = std::max(1L, 4 * rounds * slots / (4 * nin + 2 * r4));
@@ -922,7 +922,7 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
 // the wall split (variant bit 1): two cells per lane in the inner chunks; f32 at three waves per
 // SIMD, f64 at one
 template <typename T, int VS>
-constexpr bool wall_split_built() { return VS == 2; }
+constexpr bool wall_split_built() { return VS == 2 || VS == 1; }
 
 template <typename T, int VS, int K, bool SLAB>
 static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEvent_t stop, hipEvent_t start) {
@@ -935,13 +935,13 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
         // row (two-cell lanes of the inner chunks never straddle it) holding the last OWN1 or fewer rows
         constexpr int OWN1 = 64 - 2 * ghost_lanes<K, 1>();
         const int top = (a.L.ny - OWN1 + 1) & ~1;
-        if ((a.variant & 2) && a.col_step <= 0 && a.nskip == 0 && top > OWN1) {
+        if ((a.variant & 2) && (VS == 2 || (a.variant & 64)) && a.col_step <= 0 && a.nskip == 0 && top > OWN1) {
             b.wall_top = top;
             b.wall_ch0 = (top - OWN1 + rows_per_wave - 1) / rows_per_wave;
             // bit 3: the inner chunks packed, two waves per SIMD (the packed inner walk needs 191 VGPRs;
             // forced to three waves it spills 21 dwords: 0.417 vs 0.323 ms per M f32 launch, profiles/r04/pack)
-            constexpr int WPE = sizeof(T) == 4 ? 3 : 1;
-            if constexpr (sizeof(T) == 4)
+            constexpr int WPE = sizeof(T) == 4 ? (VS == 2 ? 3 : 4) : (VS == 2 ? 1 : 2);
+            if constexpr (sizeof(T) == 4 && VS == 2)
                 if (a.variant & 8)
                     return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PACK, K, SLAB, 2>(b, s, stop, start);
             if (a.variant & 32)
