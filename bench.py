@@ -4,9 +4,9 @@
 
 One step = one reference iteration (main.cu:852-909) over the whole 4096 x 4096 channel
 (periodic x, bounce-back / mirror walls, TRT + Guo forcing, uniform body force, no IB): one
-deep sweep launch (pull-stream + collide K = 5 times, intermediate states in registers,
-lbm_sweep_impl.h) per five steps and slab.  N > 1: x-slab decomposition of the SAME 4096^2
-lattice (strong scaling), one process per GPU; per 5-iteration cycle a K-column ghost exchange
+deep sweep launch (pull-stream + collide K = 6 times, intermediate states in registers,
+lbm_sweep_impl.h) per six steps and slab.  N > 1: x-slab decomposition of the SAME 4096^2
+lattice (strong scaling), one process per GPU; per K-iteration cycle a K-column ghost exchange
 via RCCL and the boundary sweeps run on a comm stream beside the interior sweep; `--scaling weak`
 gives every rank the configured width instead ((nx*N) x ny).
 
@@ -227,6 +227,12 @@ def pmc_traffic(workload_key):
     return e.get("hbm_bytes_per_launch"), e.get("source")
 
 
+
+def deep_label(mean):
+    """K of the deep launches: one depth, or the two depths a call mixed (K-1 and K)."""
+    lo, hi = int(mean), -(-mean // 1)
+    return str(int(mean)) if lo == hi else f"{lo}/{int(hi)}"
+
 def main():
     a = parse()
     # Libraries (RCCL's version banner, torch) may print to fd 1: route it to stderr and keep
@@ -331,6 +337,9 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     tm = lat.timing(reset=True)
+    # deep launches of the timed region and their mean depth (a call mixes depths K and K-1 so that
+    # it needs no remainder launches, ctx_step.hip:deep_depth)
+    deep_mean = tm["deep_iterations"] / tm["deep_launches"] if tm["deep_launches"] else float(tm["sweepk_depth"])
     if not events_in_timed and not a.no_profile_events:
         lat.set_profiling(True)
         drv.run(min(a.steps, 100))
@@ -363,7 +372,7 @@ def main():
         sweep = int(tm["sweepk_depth"])
         launch_ms = tm["sweepk_ms"] / tm["sweepk_launches"]
         cells_per_launch = tm["sweepk_cells"] // tm["sweepk_launches"]
-        iters_per_launch = sweep
+        iters_per_launch = round(deep_mean, 3)
     if a.no_profile_events:  # nothing timed per launch: name the kernel from what ran
         # (the band-cycle counter is kept without events; a deep run without IB shows as no
         # one-step launches at all, since only the boot iteration and remainders are one-step)
@@ -374,7 +383,7 @@ def main():
             sweep = 2
         else:
             sweep = False
-        iters_per_launch = sweep or 1
+        iters_per_launch = (round(deep_mean, 3) if sweep and sweep >= 3 else sweep) or 1
         launch_ms, cells_per_launch = 0.0, 0
     if distributed:
         sl = torch.tensor([launch_ms], dtype=torch.float64, device=red_dev)
@@ -418,7 +427,7 @@ def main():
             "config": {
                 "workload": f"{wdesc} ({nx}x{ny}): D2Q9 channel (periodic x, bounce-back y=0, mirror y=Y-1), "
                             f"TRT+Guo, reference TAU/TAU2; "
-                            + (f"{iters_per_launch} iterations per launch (pull-stream+collide {iters_per_launch} times, "
+                            + (f"{deep_label(iters_per_launch)} iterations per launch (pull-stream+collide K times, "
                                "intermediate states in registers)" if sweep else
                                "one fused pull-stream+collide launch per step")
                             + ((f"; IB: {ns} Lagrangian points, interpolate+spread every step, " +
@@ -455,7 +464,7 @@ def main():
                 "unit": "GB/s",
                 "frac": None if achieved is None else round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": (f"sweepk_kernel<K={iters_per_launch}> (lbm_sweep_impl.h): {iters_per_launch} iterations per "
+                "kernel": (f"sweepk_kernel<K={deep_label(iters_per_launch)}> (lbm_sweep_impl.h): {iters_per_launch} iterations per "
                            "launch, state read and written once"
                            + (" (slab interior; boundary sweeps on the comm stream)" if world > 1 or a.rccl_self else "")
                            if iters_per_launch > 2 else

@@ -194,6 +194,7 @@ struct iblb_ctx {
     long long fused_launches = 0, fused_cells = 0, sweep_launches = 0, sweep_cells = 0, sweepk_launches = 0,
               sweepk_cells = 0;
     long long band_cycles = 0, band_merged_cycles = 0, band_par_cycles = 0;  // IB band cycles run (counted without events too)
+    long long deep_launches = 0, deep_iterations = 0;  // deep launches and the iterations they advanced (no events needed)
     struct EvRec { int kind; size_t idx; long long cells; };
     std::vector<EvRec> ev_kind;
     std::string err;

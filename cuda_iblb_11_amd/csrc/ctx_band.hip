@@ -399,6 +399,8 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     int rc = ev_begin(c, &ev, ds);
     if (rc) return rc;
     HIP_TRY(c, launch_sweepk<T>(d, K, false, ds, c->band_par ? c->ev_deep : nullptr));
+    c->deep_launches++;
+    c->deep_iterations += K;
     return ev_end(c, ev, EV_SWEEPK, (long long)n * c->ny, ds);
 }
 

@@ -330,9 +330,9 @@ static int sweep_step(iblb_ctx* c) {
     return IBLB_OK;
 }
 
-// K = sweep_depth iterations in one launch on a lone slab
+// K = d iterations in one launch on a lone slab
 template <typename T>
-static int sweepk_step(iblb_ctx* c) {
+static int sweepk_step(iblb_ctx* c, int d) {
     const int W = std::max(1, c->deep_w);
     // balanced sweep widths (col_step 0: the launcher sizes the sweeps to whole rounds of waves)
     Sweep2Args<T> a = sweep_args<T>(c, 0, c->deep_balance ? 0 : W, c->ncol, (c->ncol + W - 1) / W, W);
@@ -342,13 +342,15 @@ static int sweepk_step(iblb_ctx* c) {
     hipEvent_t e0, e1;  // timing on the launch's own signals (profiling only)
     int rc = ev_kernel(c, &ev, &e0, &e1);
     if (rc) return rc;
-    HIP_TRY(c, launch_sweepk<T>(a, c->sweep_depth, false, c->stream, e1, e0));
+    HIP_TRY(c, launch_sweepk<T>(a, d, false, c->stream, e1, e0));
     if ((rc = ev_kernel_end(c, ev, EV_SWEEPK, (long long)c->ncol * c->ny))) return rc;
-    after_sweep(c, c->sweep_depth);
+    after_sweep(c, d);
+    c->deep_launches++;
+    c->deep_iterations += d;
     return IBLB_OK;
 }
 
-// K = sweep_depth iterations per cycle on a slab of an RCCL group (ncol >= 2K): K ghost columns
+// K = d iterations per cycle on a slab of an RCCL group (ncol >= 2K): K ghost columns
 // exchanged and the boundary sweeps (output columns [0, K) and [ncol-K, ncol), which read columns
 // -K .. 2K-1 and ncol-2K .. ncol+K-1) on the comm stream beside the interior sweep [K, ncol-K):
 //   compute: (join_comm: boundary(t-K)) -> interior(t) -> ev_int
@@ -360,9 +362,11 @@ static int sweepk_step(iblb_ctx* c) {
 // microseconds, profiles/r02q_*); the interior's event alternates between ev_int and ev_int2, so
 // the comm stream's waits still name interior(t-K) while interior(t) is in flight.
 // (IBLB_OVERLAP=0: exchange, boundary and interior in sequence on the compute stream.)
+// K may differ from the previous cycle's (deep_depth): the exchange waits for the previous interior
+// when it sends columns that interior wrote (comm_ready: K > bnd_w), and every ghost column read is
+// within gc = 3 sweep_depth.
 template <typename T>
-static int deep_slab_step(iblb_ctx* c) {
-    const int K = c->sweep_depth;
+static int deep_slab_step(iblb_ctx* c, int K) {
     const int W = std::max(1, c->deep_w);
     const bool ov = c->overlap;
     int rc = join_comm(c);
@@ -411,6 +415,8 @@ static int deep_slab_step(iblb_ctx* c) {
         c->deep_chain = true;
     }
     after_sweep(c, K);
+    c->deep_launches++;
+    c->deep_iterations += K;
     c->deep_chain_t = c->t;
     c->deep_chain_cur = c->cur;
     return IBLB_OK;
@@ -484,6 +490,18 @@ using namespace iblbh;
 
 extern "C" {
 
+// Depth of the next deep launch without IB, r >= K-1 iterations left in the call: K, or K-1 where
+// launches of K-1 (j of them) leave a multiple of K, so that r = j (K-1) + m K needs no two-iteration
+// or one-step remainder (every r >= (K-1)(K-2) qualifies: 20 = 4 x 5 at K = 6, 500 = 4 x 5 + 80 x 6).
+// A remainder costs more than the depth: M f64 20 iterations at K = 6 as 3 x 6 + 2 took 0.111 ms per
+// iteration against 0.097 as 4 x 5 (profiles/r04/depth).
+static int deep_depth(const iblb_ctx* c, int r) {
+    const int K = c->sweep_depth;
+    if (K < 4) return K;
+    const int j = (K - r % K) % K;
+    return (j > 0 && (long)j * (K - 1) <= r) ? K - 1 : K;
+}
+
 // nsteps iterations by the fastest applicable schedule per iteration (band cycles, deep sweeps,
 // two-iteration sweeps, one-step iterations); the band streams may still run at the end
 static int step_range(iblb_ctx* c, int nsteps) {
@@ -506,15 +524,16 @@ static int step_range(iblb_ctx* c, int nsteps) {
             continue;
         }
         if ((rc = band_join(c))) return rc;
-        if (K >= 3 && nsteps - s >= K && sweep_ready(c)) {
+        const int d = nsteps - s >= K - 1 ? deep_depth(c, nsteps - s) : K;
+        if (d >= 3 && nsteps - s >= d && sweep_ready(c)) {
             if (single_slab(c)) {
-                if ((rc = is_f64(c) ? sweepk_step<double>(c) : sweepk_step<float>(c))) return rc;
-                s += K;
+                if ((rc = is_f64(c) ? sweepk_step<double>(c, d) : sweepk_step<float>(c, d))) return rc;
+                s += d;
                 continue;
             }
-            if (rccl_multi(c) && c->ncol >= 2 * K) {
-                if ((rc = is_f64(c) ? deep_slab_step<double>(c) : deep_slab_step<float>(c))) return rc;
-                s += K;
+            if (rccl_multi(c) && c->ncol >= 2 * d) {
+                if ((rc = is_f64(c) ? deep_slab_step<double>(c, d) : deep_slab_step<float>(c, d))) return rc;
+                s += d;
                 continue;
             }
         }

@@ -151,6 +151,11 @@ typedef struct iblb_timing {
     long long band_cycles;
     long long band_merged_cycles;
     long long band_par_cycles;  /* of those, run with the last level beside the deep sweep (lone slab) */
+    /* deep launches (lone slab, slab interiors, band cycles) and the iterations they advanced, counted
+     * whether or not profiling events are on: a call of n iterations mixes depths K and K-1 so that
+     * no two-iteration or one-step remainder is left where n allows it (ctx_step.hip:deep_depth) */
+    long long deep_launches;
+    long long deep_iterations;
 } iblb_timing;
 
 /* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */

@@ -36,10 +36,11 @@ NX, NY = 8192, 2048
 
 def main():
     n, kind = int(sys.argv[1]), sys.argv[2]
-    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 21
+    K = int(os.environ.get("IBLB_SWEEP_DEPTH", "6"))  # the library's deep-sweep depth
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 1 + 4 * K
     ib = kind == "K5"
     prec = "f32" if ib else "f64"
-    chunks = [1, 10, steps - 11] if steps > 11 else [1, steps - 1]
+    chunks = [1, 2 * K, steps - 1 - 2 * K] if steps > 1 + 2 * K else [1, steps - 1]
     lib = L.load_from(os.path.join(HERE, "libiblb_mockrccl.so"))
     rho, u = W.perturbed_state(NX, NY, 29)
     pts = (lambda it: W.filament_array(it, NX, n_fil=64, pts=96, period=200, x_offset=0.0)) if ib else None
@@ -134,7 +135,7 @@ def main():
         ok = ok and t1["band_cycles"] > 0 and all(rk["band_cycles"] == t1["band_cycles"] for rk in ranks)
     else:
         ok = exact and max(d_oracle.values()) <= 1e-9 and d_q <= 1e-12
-        ok = ok and all(rk["sweepk_launches"] >= (steps - 1) // 5 for rk in ranks)
+        ok = ok and all(rk["sweepk_launches"] >= (steps - 1) // K for rk in ranks)
     print(json.dumps({"ok": bool(ok), "n": n, "workload": kind, "steps": steps, "exact": exact,
                       "d_oracle": d_oracle, "d_single": d_single, "d_single_oracle": d_single_oracle,
                       "d_flux_single": d_q, "single_band_cycles": t1["band_cycles"],

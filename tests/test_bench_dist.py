@@ -40,7 +40,7 @@ def test_bench_two_ranks(gpu, workload):
     assert d["value"] > 0 and d["ms_per_step"] > 0
     r = d["roofline"]
     assert r["frac"] is not None and r["achieved"] > 0 and r["launch_ms"] > 0
-    assert r["kernel"].startswith("sweepk_kernel<K=5>") and "slab interior" in r["kernel"], r["kernel"]
+    assert r["kernel"].startswith("sweepk_kernel<K=") and "slab interior" in r["kernel"], r["kernel"]
     assert "MAX over ranks" in r["launch_timing"]
     if workload == "K5":
         assert d["ib_band"] is not None and d["ib_band"]["deep_ms_per_cycle"] > 0  # the band cycle ran
@@ -52,5 +52,5 @@ def test_bench_two_ranks(gpu, workload):
 def test_bench_labels_without_events(gpu):
     d = _run(["--workload", "M", "--steps", "20", "--warmup", "5", "--no-profile-events"])
     r = d["roofline"]
-    assert r["frac"] is None and r["kernel"].startswith("sweepk_kernel<K=5>") and "not timed" in r["kernel"]
+    assert r["frac"] is None and r["kernel"].startswith("sweepk_kernel<K=") and "not timed" in r["kernel"]
     assert r["launch_timing"].startswith("none")

@@ -20,6 +20,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 TOL64, TOL32, TIGHT = 1e-6, 1e-4, 1e-9
+# the library's deep-sweep depth (IBLB_SWEEP_DEPTH, default 6): the step counts below are built from
+# it, so that "boot + two deep launches" is 1 + 2K iterations whatever K is
+K = int(os.environ.get("IBLB_SWEEP_DEPTH", "6"))
+CHUNKS = [1, 2 * K + 2, K, 3, 3 * K]  # boot, two cycles + 2, one cycle, 3 one-step, three cycles
 
 
 def rel(a, b):
@@ -59,10 +63,10 @@ def bulk_pair(P, O, nx, ny, chunks, *, precision="f64", seed=31):
 
 
 def test_k1_1000_steps_bulk(gpu, oracle, threads):
-    """K1: 128 x 128, 1000 iterations in one call (boot + 199 deep launches + remainder): the
-    longest horizon of the deep sweep against the restatement."""
+    """K1: 128 x 128, 1000 iterations in one call (boot + ~999/K deep launches of depths K and
+    K-1, no remainder): the longest horizon of the deep sweep against the restatement."""
     lat, sim, tm = bulk_pair(gpu, oracle, 128, 128, [1000])
-    assert tm["sweepk_launches"] >= 190, tm
+    assert tm["sweepk_launches"] >= 999 // K - 1 and tm["deep_iterations"] == 999, tm
     r = fields(lat, sim)
     assert max(r["rho"], r["ux"], r["uy"]) <= TIGHT, r
     assert r["rho-1"] <= 1e-8, r
@@ -70,8 +74,8 @@ def test_k1_1000_steps_bulk(gpu, oracle, threads):
 
 
 def test_k2_bulk(gpu, oracle, threads):
-    """K2: 2048^2 f64, 23 iterations in chunks that mix deep launches and remainders."""
-    lat, sim, tm = bulk_pair(gpu, oracle, 2048, 2048, [1, 10, 7, 5])
+    """K2: 2048^2 f64, 4K + 3 iterations in chunks that mix deep launches and remainders."""
+    lat, sim, tm = bulk_pair(gpu, oracle, 2048, 2048, [1, 2 * K, K + 2, K])
     assert tm["sweepk_launches"] >= 3, tm
     r = fields(lat, sim)
     assert max(r["rho"], r["ux"], r["uy"]) <= TIGHT, r
@@ -79,8 +83,8 @@ def test_k2_bulk(gpu, oracle, threads):
 
 
 def test_k4_bulk(gpu, oracle, threads):
-    """K4: 8192 x 2048 f64 (one GPU), 11 iterations: boot + two deep launches."""
-    lat, sim, tm = bulk_pair(gpu, oracle, 8192, 2048, [11])
+    """K4: 8192 x 2048 f64 (one GPU), 1 + 2K iterations: boot + two deep launches."""
+    lat, sim, tm = bulk_pair(gpu, oracle, 8192, 2048, [1 + 2 * K])
     assert tm["sweepk_launches"] == 2, tm
     r = fields(lat, sim)
     assert max(r["rho"], r["ux"], r["uy"]) <= TIGHT, r
@@ -88,8 +92,8 @@ def test_k4_bulk(gpu, oracle, threads):
 
 
 def test_m_bulk_perturbed(gpu, oracle, threads):
-    """M: 4096^2 f64 (the metric config) from a perturbed, not x-uniform, state, 11 iterations."""
-    lat, sim, tm = bulk_pair(gpu, oracle, 4096, 4096, [11])
+    """M: 4096^2 f64 (the metric config) from a perturbed, not x-uniform, state, 1 + 2K iterations."""
+    lat, sim, tm = bulk_pair(gpu, oracle, 4096, 4096, [1 + 2 * K])
     assert tm["sweepk_launches"] == 2, tm
     r = fields(lat, sim)
     assert max(r["rho"], r["ux"], r["uy"]) <= TIGHT, r
@@ -109,12 +113,12 @@ def _record(name, r):
 
 
 def test_m_bulk_f32(gpu, oracle, threads):
-    """M in f32, 11 iterations (boot + two deep launches); rho - 1 and u each normalised by their
+    """M in f32, 1 + 2K iterations (boot + two deep launches); rho - 1 and u each normalised by their
     own max (f32 stores f - w_i, so rho - 1 is resolved, not rho ~ 1)."""
-    lat, sim, tm = bulk_pair(gpu, oracle, 4096, 4096, [11], precision="f32")
+    lat, sim, tm = bulk_pair(gpu, oracle, 4096, 4096, [1 + 2 * K], precision="f32")
     assert tm["sweepk_launches"] == 2, tm
     r = fields(lat, sim)
-    _record("M_4096_f32_11", r)
+    _record(f"M_4096_f32_{1 + 2 * K}", r)
     assert max(r["rho-1"], r["ux"], r["uy"]) <= TOL32, r
 
 
@@ -125,13 +129,15 @@ def test_k1_1000_steps_bulk_f32(gpu, oracle, threads):
     numpy float32 restatement (tests/f32_model.py) lands at 1.5e-4 on rho - 1 and u_y.  The kernels'
     f32 collide takes the odd equilibrium part from the momentum and never multiplies by the
     float32-rounded rho (iblb_device.h collide_sd, JM): 7.9e-5 / 3.6e-5 in the CPU emulation of the
-    same arithmetic (tests/f32_gpu_model.py; the round-3 order measured 1.8e-4 on rho - 1)."""
+    same arithmetic (tests/f32_gpu_model.py; the round-3 order measured 1.8e-4 on rho - 1).
+    (The deep launches' depth does not change a cell's arithmetic: every depth is bit-identical to
+    one-step launches, test_sweep_deep_bit_identical.)"""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from f32_model import F32Channel
     from cuda_iblb_11_amd import workloads as W
     lat, sim, tm = bulk_pair(gpu, oracle, 128, 128, [1000], precision="f32")
-    assert tm["sweepk_launches"] >= 190, tm
+    assert tm["sweepk_launches"] >= 999 // K - 1, tm
     r = fields(lat, sim)
     rho, u = W.perturbed_state(128, 128, 31)
     m = F32Channel(128, 128, W.TAU, W.TAU2, rho, u, W.BODY_FORCE)
@@ -151,7 +157,7 @@ def test_band_cycle_f32_100_steps(gpu, oracle, threads):
     from cuda_iblb_11_amd import workloads as W
     pts = lambda it: W.filament(it, n_points=256, x0=1024.3, y0=1.0, dy=1.0, U0=2e-3, period=40, sway=2.0)
     lat, sim = moving_run(gpu, oracle, 2048, 2048, pts, [25, 25, 25, 25], precision="f32", body_force=W.BODY_FORCE)
-    assert lat.timing()["sweepk_launches"] >= 18
+    assert lat.timing()["sweepk_launches"] >= 4 * (25 // K) - 2
     r = fields(lat, sim)
     _record("band_2048_f32_100_moving", r)
     assert max(r["rho-1"], r["ux"], r["uy"]) <= TOL32, r
@@ -215,7 +221,7 @@ def test_moving_points_band_cycle_matches_oracle(gpu, oracle, precision, monkeyp
     """Points that move every iteration through the IB band cycle: the schedule's forced columns
     make the bands, each level's IB uses its own iteration's points; readers between chunks."""
     nx, ny = 320, 128
-    lat, sim = moving_run(gpu, oracle, nx, ny, _swaying(nx), [1, 12, 5, 3, 15], precision=precision,
+    lat, sim = moving_run(gpu, oracle, nx, ny, _swaying(nx), CHUNKS, precision=precision,
                           monkeypatch=monkeypatch, readers=True)
     tm = lat.timing()
     assert tm["sweepk_launches"] >= 6, tm  # band cycles ran (one deep sweep each)
@@ -258,11 +264,11 @@ def test_schedule_equals_per_iteration_points(gpu, oracle, monkeypatch):
 
 def test_k3_time_varying_filament(gpu, oracle, threads):
     """K3 as SURVEY.md §8(d) prescribes it: 2048^2 f64, one 256-point filament at x = 1024 with
-    u_s(it) = (U0 (k/255) sin(2 pi it / T), 0) changing every iteration; 12 iterations in one
+    u_s(it) = (U0 (k/255) sin(2 pi it / T), 0) changing every iteration; 2K + 2 iterations in one
     call through the band cycle."""
     from cuda_iblb_11_amd import workloads as W
     pts = lambda it: W.filament(it, n_points=256, x0=1024.0, y0=1.0, dy=1.0, U0=1e-3, period=20)
-    lat, sim = moving_run(gpu, oracle, 2048, 2048, pts, [12])
+    lat, sim = moving_run(gpu, oracle, 2048, 2048, pts, [2 * K + 2])
     assert lat.timing()["sweepk_launches"] >= 2
     r = fields(lat, sim)
     assert max(r["rho"], r["ux"], r["uy"]) <= 1e-10, r
@@ -272,14 +278,14 @@ def test_k3_time_varying_filament(gpu, oracle, threads):
 def test_k5_filament_array_f32(gpu, oracle, threads):
     """K5 on one GPU: 8192 x 2048 f32 + 64 filaments x 96 points (6144) that move every
     iteration, one on every slab edge of an 8-slab split (x = 0 included, the filament there
-    crosses it: ghost-column trapezoids), 11 iterations in one call: boot + two band cycles;
+    crosses it: ghost-column trapezoids), 1 + 2K iterations in one call: boot + two band cycles;
     rho - 1 and u each normalised by its own max."""
     from cuda_iblb_11_amd import workloads as W
     pts = lambda it: W.filament_array(it, 8192, n_fil=64, pts=96, period=200, x_offset=0.0)
-    lat, sim = moving_run(gpu, oracle, 8192, 2048, pts, [11], precision="f32", body_force=W.BODY_FORCE)
+    lat, sim = moving_run(gpu, oracle, 8192, 2048, pts, [1 + 2 * K], precision="f32", body_force=W.BODY_FORCE)
     assert lat.timing()["sweepk_launches"] == 2
     r = fields(lat, sim)
-    _record("K5_8192x2048_f32_11_edges", r)
+    _record(f"K5_8192x2048_f32_{1 + 2 * K}_edges", r)
     assert max(r["rho-1"], r["ux"], r["uy"]) <= TOL32, r
 
 
@@ -301,7 +307,7 @@ def test_band_streams_keep_the_context_stream(gpu, monkeypatch):
     stream0 = lat.stream
     lat.set_lagrangian(s, us)
     lat.set_profiling(True)
-    lat.step(11)  # boot + two band cycles
+    lat.step(1 + 2 * K)  # boot + two band cycles
     assert lat.timing(reset=True)["sweepk_launches"] == 2  # the band cycle ran on its streams
     assert lat.stream == stream0
     lat.set_lagrangian(np.zeros(0, np.float32), np.zeros(0, np.float32))  # points gone
@@ -310,12 +316,12 @@ def test_band_streams_keep_the_context_stream(gpu, monkeypatch):
     ref2 = gpu.Lattice(nx, ny, W.TAU, W.TAU2, body_force=W.BODY_FORCE, max_points=30)
     ref2.set_state(rho, u)
     ref2.set_lagrangian(s, us)
-    ref2.step(11)
+    ref2.step(1 + 2 * K)
     ref2.set_lagrangian(np.zeros(0, np.float32), np.zeros(0, np.float32))
-    lat.step(25)
-    ref2.step(25)
+    lat.step(1 + 4 * K)
+    ref2.step(1 + 4 * K)
     # the first iteration still consumes the force the old points owe (one-step launch), then
-    # 4 deep launches + 2 two-iteration launches
+    # 4 deep launches
     assert lat.timing()["sweepk_launches"] == 4
     r1, u1 = lat.macro()
     r2, u2 = ref2.macro()
@@ -380,7 +386,7 @@ def test_moving_points_across_x0(gpu, oracle, precision, monkeypatch):
     """Filaments swaying across x = 0 through the lone slab's band cycle (ghost columns filled by
     periodic copies every cycle), against the oracle."""
     nx, ny = 256, 128
-    lat, sim = moving_run(gpu, oracle, nx, ny, _crossing(nx), [1, 12, 5, 3, 15], precision=precision,
+    lat, sim = moving_run(gpu, oracle, nx, ny, _crossing(nx), CHUNKS, precision=precision,
                           monkeypatch=monkeypatch, readers=True)
     assert lat.timing()["sweepk_launches"] >= 6
     r = fields(lat, sim)
@@ -399,7 +405,7 @@ def test_ib_band_par_equals_serial(gpu, oracle, precision, merge, monkeypatch):
     out = {}
     for par in ("2", "0"):  # always / never (the default, 1, picks it where the deep sweep is short)
         monkeypatch.setenv("IBLB_BAND_PAR", par)
-        lat, sim = moving_run(gpu, oracle, nx, ny, _crossing(nx), [1, 12, 5, 3, 15], precision=precision,
+        lat, sim = moving_run(gpu, oracle, nx, ny, _crossing(nx), CHUNKS, precision=precision,
                               monkeypatch=monkeypatch, readers=True)
         tm = lat.timing()
         assert tm["band_cycles"] >= 6 and (tm["band_par_cycles"] == tm["band_cycles"]) == (par == "2"), tm

@@ -9,12 +9,17 @@ restatement at the 1e-16 level per step; the tests also assert a much tighter en
 bound (TIGHT) so that any semantic slip (a wrong boundary rule, a lagged force, a missing
 flux term) is caught long before it could hide under 1e-6.
 """
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 TOL64, TOL32, TIGHT = 1e-6, 1e-4, 1e-9
+# the library's deep-sweep depth (IBLB_SWEEP_DEPTH, default 6): the band tests' step counts are built
+# from it (a chunk of n >= K iterations runs n // K band cycles)
+K = int(os.environ.get("IBLB_SWEEP_DEPTH", "6"))
 
 
 def rel(a, b):
@@ -347,7 +352,7 @@ def test_rccl_slab_band_cycle_threads_chain(gpu, n, precision, merge, monkeypatc
                                               (8, "K5", "0"), (2, "K5", "2")])
 def test_full_size_decomposed(gpu, n, workload, merge):
     """BASELINE configs 4 and 5 decomposed at their real size, 8192 x 2048 over 2 / 4 / 8 ranks
-    (mock RCCL: ranks as threads on one GPU), 21 iterations in bulk calls (boot + 4 cycles), against
+    (mock RCCL: ranks as threads on one GPU), 1 + 4K iterations in bulk calls (boot + 4 cycles), against
     the lone slab and the oracle (tests/mock_rccl/run_full.py).  K4 f64: bit-identical to the lone
     slab, <= 1e-9 vs the oracle.  K5 f32 + 64 filaments x 96 points on every slab edge (x = 0
     included), moving every iteration: the IB band cycle on every rank, <= 1e-4 vs the oracle.
@@ -410,12 +415,12 @@ def test_reference_cilia_scenario(gpu, oracle, precision):
 def test_cilia_band_cycle(gpu, oracle, precision, monkeypatch):
     """On-device cilia through the IB band cycle (round 3): iblb_step runs the kinematics of the
     call's iterations ahead as a schedule and then K iterations per cycle.  8 cilia 128 apart on
-    1024 x 192, 23 iterations in chunks (1, 20, 2): boot, four band cycles, one-step remainders with
+    1024 x 192, 4K + 3 iterations in chunks (1, 4K, 2): boot, four band cycles, one-step remainders with
     the kinematics launched per iteration again; against the oracle fed by the restated kinematics
     and against the one-step path (IBLB_IB_BAND=0)."""
     from cuda_iblb_11_amd import workloads as W
     c_num, c_space, T = 8, 128.0, 100000
-    nx, ny, steps = int(c_num * c_space), 192, 23
+    nx, ny, steps = int(c_num * c_space), 192, 4 * K + 3
     p_step = T // c_num
     sim = oracle.Simulation(nx, ny, W.TAU, W.TAU2)
     cil = oracle.Cilia(c_num, c_space, T, p_step, nx)
@@ -429,7 +434,7 @@ def test_cilia_band_cycle(gpu, oracle, precision, monkeypatch):
         lat.set_state()
         lat.set_cilia(c_num, c_space, T, p_step)
         lat.set_profiling(True)
-        for n in (1, 20, 2):
+        for n in (1, 4 * K, 2):
             lat.step(n)
         s_g, us_g, eps_g = lat.lagrangian()
         assert np.array_equal(s_g, cil.s) and np.array_equal(us_g, cil.u_s) and np.array_equal(eps_g, cil.epsilon)
@@ -588,10 +593,15 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
     their own sweep family of the three-wave build; 8, 9, 11: the packed two-cell collide, 11 with
     the wall chunks split off), wave order and walking direction, on
     ragged shapes including fewer columns than the K-column reach (periodic images wrap more
-    than once).  1 + 10K + 2 steps = boot + 10 deep launches + one two-iteration launch."""
+    than once).  Calls of 1 + 10K, 2 and 2K - 1 iterations: boot + 10 deep launches, one
+    two-iteration launch, then (K >= 4) one launch of depth K - 1 and one of depth K (a call mixes
+    the two so that it needs no remainder, ctx_step.hip:deep_depth; K = 3: one deep launch and a
+    two-iteration one)."""
     from cuda_iblb_11_amd import workloads as W
     vss = [2, 1]
-    steps = 1 + 10 * depth + 2
+    calls = [1 + 10 * depth, 2, 2 * depth - 1]
+    steps = sum(calls)
+    n_deep, n_two = (12, 1) if depth >= 4 else (11, 2)
     for nx, ny in [(37, 300), (2, 63), (5, 1100), (70, 125), (3, 130)]:
         rho, u = W.perturbed_state(nx, ny, 7)
         monkeypatch.setenv("IBLB_SWEEP", "0")
@@ -612,9 +622,11 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
                 lat = gpu.Lattice(nx, ny, W.TAU, W.TAU2, precision=precision, body_force=(1e-6, 3e-7))
                 lat.set_state(rho, u)
                 lat.set_profiling(True)
-                lat.step(steps)
+                for n in calls:
+                    lat.step(n)
                 tm = lat.timing()
-                assert tm["sweepk_launches"] == 10 and tm["sweep_launches"] == 1 and tm["sweepk_depth"] == depth, tm
+                assert tm["sweepk_launches"] == n_deep and tm["sweep_launches"] == n_two, tm
+                assert tm["sweepk_depth"] == depth and tm["deep_iterations"] == steps - 1 - 2 * n_two, tm
                 f = lat.populations()
                 assert np.array_equal(f, f_ref), (nx, ny, vs, w, var, bal,
                                                   float(np.max(np.abs(f - f_ref))))
@@ -705,12 +717,12 @@ def _line(xs, n, y0=3.0, dy=1.0, amp=1.5e-3):
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_ib_band_cycle_matches_oracle(gpu, oracle, precision, monkeypatch):
-    """Two filaments (two bands, one deep gap each side), 1 + 5*6 + 2 steps in one call: boot,
-    six band cycles, a one-step remainder; fields, force, F_s and the flux against the oracle."""
+    """Two filaments (two bands, one deep gap each side), 1 + 6K + 2 steps in one call: boot,
+    six band cycles, one-step remainders; fields, force, F_s and the flux against the oracle."""
     nx, ny = 256, 160
     a, b = _line(64.37, 60), _line(171.6, 48, y0=20.0)
     pts = tuple(np.concatenate([p, q]) for p, q in zip(a, b))
-    lat, sim = _static_run(gpu, oracle, nx, ny, 33, pts, precision=precision, monkeypatch=monkeypatch)
+    lat, sim = _static_run(gpu, oracle, nx, ny, 1 + 6 * K + 2, pts, precision=precision, monkeypatch=monkeypatch)
     tm = lat.timing()
     assert tm["sweepk_launches"] >= 6, tm  # the band cycle ran (one deep sweep per cycle)
     tol = 1e-10 if precision == "f64" else TOL32
@@ -731,7 +743,8 @@ def test_ib_band_stream_arrangements(gpu, oracle, band_cus, monkeypatch):
     nx, ny = 256, 160
     a, b = _line(64.37, 60), _line(171.6, 48, y0=20.0)
     pts = tuple(np.concatenate([p, q]) for p, q in zip(a, b))
-    lat, sim = _static_run(gpu, oracle, nx, ny, 38, pts, chunks=(1, 10, 12, 15), monkeypatch=monkeypatch)
+    lat, sim = _static_run(gpu, oracle, nx, ny, 7 * K + 3, pts, chunks=(1, 2 * K, 2 * K + 2, 3 * K),
+                           monkeypatch=monkeypatch)
     assert lat.timing()["sweepk_launches"] >= 6
     check_fields(lat, sim, 1e-10)
     assert abs(lat.flux - sim.flux) <= 1e-9 * max(abs(sim.flux), 1e-30)
@@ -742,7 +755,7 @@ def test_ib_band_flux_column(gpu, oracle, x0, monkeypatch):
     """Flux column XDIM-5 = 251 inside a band's output (x0 = 246), inside its trapezoid ghost
     columns only (x0 = 244: the deep sweep adds it, the ghosts must not), and in a gap."""
     nx, ny = 256, 128
-    lat, sim = _static_run(gpu, oracle, nx, ny, 20, _line(x0, 40), monkeypatch=monkeypatch)
+    lat, sim = _static_run(gpu, oracle, nx, ny, 3 * K + 2, _line(x0, 40), monkeypatch=monkeypatch)
     assert lat.timing()["sweepk_launches"] >= 3
     check_fields(lat, sim, 1e-10)
     assert abs(lat.flux - sim.flux) <= 1e-9 * max(abs(sim.flux), 1e-30)
@@ -750,13 +763,13 @@ def test_ib_band_flux_column(gpu, oracle, x0, monkeypatch):
 
 def test_ib_band_equals_one_step_path(gpu, oracle, monkeypatch):
     """The band cycle against the same run with IBLB_IB_BAND=0 (one-step launches only): equal up
-    to the arrival order of the spread atomics; the chunked calls (3, 5, 7, 5, 10) interleave band
+    to the arrival order of the spread atomics; the chunked calls (3, K, K + 2, K, 2K) interleave band
     cycles, one-step remainders and readers (macro, force) between them."""
     nx, ny = 320, 96
     pts = tuple(np.concatenate([p, q, r]) for p, q, r in zip(_line(40.0, 30), _line(60.0, 30), _line(200.4, 50)))
     runs = {}
     for band in (1, 0):
-        lat, sim = _static_run(gpu, oracle, nx, ny, 30, pts, chunks=(3, 5, 7, 5, 10), band=band,
+        lat, sim = _static_run(gpu, oracle, nx, ny, 5 * K + 5, pts, chunks=(3, K, K + 2, K, 2 * K), band=band,
                                monkeypatch=monkeypatch)
         runs[band] = (lat.macro(), lat.force(), lat.flux, lat.timing()["sweepk_launches"])
         check_fields(lat, sim, 1e-10)  # each run against the oracle, the band run included
@@ -776,7 +789,7 @@ def test_ib_band_near_lattice_edges(gpu, oracle, precision, monkeypatch):
     a, b = _line(0.4, 30), _line(nx - 1.3, 24, y0=40.0)
     a[0][0::2] = np.mod(a[0][0::2], nx)  # wrapped into [0, XDIM) as boundary_check does
     pts = tuple(np.concatenate([p, q]) for p, q in zip(a, b))
-    lat, sim = _static_run(gpu, oracle, nx, ny, 22, pts, precision=precision, monkeypatch=monkeypatch)
+    lat, sim = _static_run(gpu, oracle, nx, ny, 4 * K + 2, pts, precision=precision, monkeypatch=monkeypatch)
     assert lat.timing()["sweepk_launches"] >= 4
     check_fields(lat, sim, 1e-10 if precision == "f64" else TOL32)
     assert abs(lat.flux - sim.flux) <= (1e-9 if precision == "f64" else 1e-4) * max(abs(sim.flux), 1e-30)
@@ -796,7 +809,7 @@ def test_ib_band_merged_equals_chained(gpu, oracle, precision, monkeypatch):
     runs = {}
     for merge in ("2", "0"):  # always / never (the default, 1, merges where the deep sweep is short)
         monkeypatch.setenv("IBLB_BAND_MERGE", merge)
-        lat, sim = _static_run(gpu, oracle, nx, ny, 33, pts, chunks=(1, 12, 5, 15), precision=precision,
+        lat, sim = _static_run(gpu, oracle, nx, ny, 6 * K + 3, pts, chunks=(1, 2 * K + 2, K, 3 * K), precision=precision,
                                monkeypatch=monkeypatch)
         tm = lat.timing()
         assert tm["sweepk_launches"] >= 5, tm
@@ -834,7 +847,7 @@ def test_ib_band_many_points(gpu, oracle, precision, monkeypatch):
                                                               _line(200.4, 50, y0=90.0)))
     runs, errs = {}, {}
     for band in (1, 0):
-        lat, sim = _static_run(gpu, oracle, nx, ny, 31, pts, chunks=(1, 10, 7, 13), precision=precision,
+        lat, sim = _static_run(gpu, oracle, nx, ny, 5 * K + 3, pts, chunks=(1, 2 * K, K + 1, 2 * K + 1), precision=precision,
                                monkeypatch=monkeypatch, band=band)
         tm = lat.timing()
         runs[band] = (lat.macro(), lat.force(), lat.lagrangian_force(), lat.flux, tm)
