@@ -91,8 +91,10 @@ class Driver:
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=500)
-    p.add_argument("--warmup", type=int, default=50)
+    # 480 and 60: multiples of 5 and 6, whole cycles at either deep depth (an IB band cycle run ends
+    # with one-step iterations over the whole lattice for a remainder)
+    p.add_argument("--steps", type=int, default=480)
+    p.add_argument("--warmup", type=int, default=60)
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="M",
                    help="BASELINE.json config: M (metric, default), K2..K5")
     p.add_argument("--nx", type=int, default=None)
@@ -342,7 +344,9 @@ def main():
     deep_mean = tm["deep_iterations"] / tm["deep_launches"] if tm["deep_launches"] else float(tm["sweepk_depth"])
     if not events_in_timed and not a.no_profile_events:
         lat.set_profiling(True)
-        drv.run(min(a.steps, 100))
+        # whole cycles only (an IB run's last n mod K iterations are one-step launches over the lattice)
+        kd = int(tm["sweepk_depth"])
+        drv.run(max(kd, min(a.steps, 100) // kd * kd) if kd >= 3 else min(a.steps, 100))
         lat.synchronize()
         tm = lat.timing(reset=True)
         lat.set_profiling(False)
