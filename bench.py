@@ -4,8 +4,8 @@
 
 One step = one reference iteration (main.cu:852-909) over the whole 4096 x 4096 channel
 (periodic x, bounce-back / mirror walls, TRT + Guo forcing, uniform body force, no IB): one
-deep sweep launch (pull-stream + collide K = 6 times, intermediate states in registers,
-lbm_sweep_impl.h) per six steps and slab.  N > 1: x-slab decomposition of the SAME 4096^2
+deep sweep launch (pull-stream + collide K = 7 times, intermediate states in registers,
+lbm_sweep_impl.h) per seven steps and slab (K - 1 = 6 where a call's length needs it).  N > 1: x-slab decomposition of the SAME 4096^2
 lattice (strong scaling), one process per GPU; per K-iteration cycle a K-column ghost exchange
 via RCCL and the boundary sweeps run on a comm stream beside the interior sweep; `--scaling weak`
 gives every rank the configured width instead ((nx*N) x ny).
@@ -91,10 +91,10 @@ class Driver:
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    # 480 and 60: multiples of 5 and 6, whole cycles at either deep depth (an IB band cycle run ends
-    # with one-step iterations over the whole lattice for a remainder)
-    p.add_argument("--steps", type=int, default=480)
-    p.add_argument("--warmup", type=int, default=60)
+    # 420 and 42: multiples of every deep depth 3 ... 7 (an IB band cycle run ends with one-step
+    # iterations over the whole lattice for a remainder)
+    p.add_argument("--steps", type=int, default=420)
+    p.add_argument("--warmup", type=int, default=42)
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="M",
                    help="BASELINE.json config: M (metric, default), K2..K5")
     p.add_argument("--nx", type=int, default=None)

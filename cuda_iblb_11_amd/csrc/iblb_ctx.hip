@@ -327,15 +327,16 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->max_points = cfg->max_points;
     // kernel defaults measured on MI355X: one-step variant f64 = DPP row shift +
     // nontemporal stores (5), f32 = nontemporal loads and stores (3); two-step sweeps 16 B per lane
-    // (f64 2 cells, f32 4) over 4 / 6 columns; deep sweeps K = 6 (round 4: M f64 176k vs 171k MLUPS at
-    // K = 5, f32 280k vs 255k, profiles/r04/depth), 2 cells per lane, ~96 (f64) / ~64
+    // (f64 2 cells, f32 4) over 4 / 6 columns; deep sweeps K = 7 (round 4, profiles/r04/depth: M f64
+    // 171k / 174k / 182k MLUPS at K = 5 / 6 / 7, f32 255k / 280k / 304k; K = 8 dropped), 2 cells per
+    // lane, ~96 (f64) / ~64
     // (f32) columns balanced to whole rounds of resident waves, the linear wave order dealt to the
     // XCDs in contiguous ranges (map 2) with alternate sweeps walking towards each other
     c->variant = (int)env_long("IBLB_FUSED_VARIANT", f64 ? 5 : 3);
     c->sweep_on = env_long("IBLB_SWEEP", 1) != 0;
     c->sweep_w = (int)env_long("IBLB_SWEEP_W", f64 ? 4 : 6);
     c->sweep_vs = (int)env_long("IBLB_SWEEP_VS", f64 ? 2 : 4);
-    c->sweep_depth = (int)std::min(6L, std::max(2L, env_long("IBLB_SWEEP_DEPTH", 6)));
+    c->sweep_depth = (int)std::min(7L, std::max(2L, env_long("IBLB_SWEEP_DEPTH", 7)));
     c->deep_w = (int)env_long("IBLB_DEEP_W", f64 ? 96 : 64);
     c->deep_vs = (int)env_long("IBLB_DEEP_VS", 2);
     // f32: the wall split (variant bit 1) with the packed collide (bit 3), profiles/r04/pack; f64: the

@@ -15,6 +15,7 @@ IBLB_SWEEPK_EXTERN_K(3)
 IBLB_SWEEPK_EXTERN_K(4)
 IBLB_SWEEPK_EXTERN_K(5)
 IBLB_SWEEPK_EXTERN_K(6)
+IBLB_SWEEPK_EXTERN_K(7)
 
 template <typename T, bool SLAB>
 static hipError_t launch_sweepk_slab(const Sweep2Args<T>& a, int depth, hipStream_t s, hipEvent_t stop,
@@ -23,6 +24,7 @@ static hipError_t launch_sweepk_slab(const Sweep2Args<T>& a, int depth, hipStrea
     if (depth == 4) return launch_sweepk_depth<T, 4, SLAB>(a, s, stop, start);
     if (depth == 5) return launch_sweepk_depth<T, 5, SLAB>(a, s, stop, start);
     if (depth == 6) return launch_sweepk_depth<T, 6, SLAB>(a, s, stop, start);
+    if (depth == 7) return launch_sweepk_depth<T, 7, SLAB>(a, s, stop, start);
     return hipErrorInvalidValue;
 }
 
@@ -36,6 +38,7 @@ int sweepk_geometry(int depth, int vs, int variant, bool slab, int ny, int* nch)
         case 4: return slab ? deep_geometry<T, 4, true>(vs, variant, ny, nch) : deep_geometry<T, 4, false>(vs, variant, ny, nch);
         case 5: return slab ? deep_geometry<T, 5, true>(vs, variant, ny, nch) : deep_geometry<T, 5, false>(vs, variant, ny, nch);
         case 6: return slab ? deep_geometry<T, 6, true>(vs, variant, ny, nch) : deep_geometry<T, 6, false>(vs, variant, ny, nch);
+        case 7: return slab ? deep_geometry<T, 7, true>(vs, variant, ny, nch) : deep_geometry<T, 7, false>(vs, variant, ny, nch);
         default: return 0;
     }
 }

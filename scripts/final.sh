@@ -4,7 +4,7 @@
 #   2. rocprofv3 kernel-trace stats of the same bench command (the dominant kernel's mean duration);
 #   3. HBM traffic (FETCH_SIZE and WRITE_SIZE in separate --pmc passes) and SQ VALU passes of the
 #      deep f64 / f32 launches -> profiles/pmc_traffic.json / pmc_valu.json (scripts/pmc_*.py);
-#   4. every BASELINE config at N = 1 (M at the driver's 20 steps and at 480, M f32, K2, K3, K4, K5);
+#   4. every BASELINE config at N = 1 (M at the driver's 20 steps and at 420, M f32, K2, K3, K4, K5);
 #   5. the multi-GPU rehearsal: the per-rank slabs of the 4096^2 strong-scaling runs (2048 / 1024 / 512
 #      columns) and the K5-width slab (1024 x 2048 f32, filaments on the slab edge / mid-slab), lone
 #      and on the RCCL self ring, 7 timed regions each inside one process (scripts/ring_reps.py).
@@ -30,23 +30,23 @@ mkdir -p "$OUT"
 B="python3 bench.py --no-cpu-baseline"
 [ -z "$SKIP_PMC" ] && {
   timeout -k 10 -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace \
-    -- $B --steps 240 --warmup 30 --prime-seconds 0.5 > "$OUT/trace_bench.json" 2> "$OUT/trace.err" || { tail -20 "$OUT/trace.err"; exit 1; }
+    -- $B --steps 210 --warmup 21 --prime-seconds 0.5 > "$OUT/trace_bench.json" 2> "$OUT/trace.err" || { tail -20 "$OUT/trace.err"; exit 1; }
   find "$OUT/trace" -name "*kernel_stats.csv" -exec head -4 {} \;
-  # the depth-6 launches only (the default; a call's K-1 launches carry the same bytes): 60 steps =
+  # the depth-7 launches only (the default; a call's K-1 launches carry the same bytes): 70 steps =
   # ten of them, the kernel named with its template arguments (f64 variant 35 -> mode 273, f32 11 -> 81)
   for prec in f64 f32; do
-    if [ $prec = f64 ]; then kn="sweepk_kernel<double, 2, 273, 6,"; else kn="sweepk_kernel<float, 2, 81, 6,"; fi
+    if [ $prec = f64 ]; then kn="sweepk_kernel<double, 2, 273, 7,"; else kn="sweepk_kernel<float, 2, 81, 7,"; fi
     for c in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 -s KILL 180 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${c}_$prec" -o pmc \
-        -- $B --precision $prec --steps 60 --warmup 6 --prime-seconds 0.3 --no-profile-events > /dev/null 2> "$OUT/pmc_${c}_$prec.err" \
+        -- $B --precision $prec --steps 70 --warmup 7 --prime-seconds 0.3 --no-profile-events > /dev/null 2> "$OUT/pmc_${c}_$prec.err" \
         || { tail -20 "$OUT/pmc_${c}_$prec.err"; exit 1; }
     done
-    python3 scripts/pmc_summary.py ${prec}_4096x4096_n1_sweep6 "$OUT/pmc_FETCH_SIZE_$prec" "$OUT/pmc_WRITE_SIZE_$prec" \
+    python3 scripts/pmc_summary.py ${prec}_4096x4096_n1_sweep7 "$OUT/pmc_FETCH_SIZE_$prec" "$OUT/pmc_WRITE_SIZE_$prec" \
       "$OUT/pmc_traffic.json" --kernel "$kn"
     fl=FP64; [ $prec = f32 ] && fl=FP32
     timeout -k 10 -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_$fl SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAVES GRBM_GUI_ACTIVE \
       --output-format csv -d "$OUT/pmc_valu_$prec" -o pmc \
-      -- $B --precision $prec --steps 60 --warmup 6 --prime-seconds 0.3 --no-profile-events > /dev/null 2> "$OUT/pmc_valu_$prec.err" \
+      -- $B --precision $prec --steps 70 --warmup 7 --prime-seconds 0.3 --no-profile-events > /dev/null 2> "$OUT/pmc_valu_$prec.err" \
       || { tail -20 "$OUT/pmc_valu_$prec.err"; exit 1; }
   done
   cat "$OUT/pmc_traffic.json"
@@ -56,12 +56,12 @@ B="python3 bench.py --no-cpu-baseline"
   run() { local name=$1; shift; timeout -k 10 300 $B "$@" > "$OUT/bench_$name.json" 2> "$OUT/bench_$name.err" || { tail -5 "$OUT/bench_$name.err"; return 1; }
           python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], d['value'], d['ms_per_step'], r['launch_ms'], r['frac'], d.get('ib_band'))" "$OUT/bench_$name.json" "$name"; }
   run M_20 --steps 20 --warmup 5 || exit 1
-  run M_480 --steps 480 --warmup 60 || exit 1
-  run M_f32 --steps 480 --warmup 60 --precision f32 || exit 1
-  run K2 --workload K2 --steps 480 --warmup 60 || exit 1
-  run K4 --workload K4 --steps 480 --warmup 60 || exit 1
-  run K3 --workload K3 --steps 480 --warmup 60 || exit 1
-  run K5 --workload K5 --steps 480 --warmup 60 || exit 1
+  run M_420 --steps 420 --warmup 42 || exit 1
+  run M_f32 --steps 420 --warmup 42 --precision f32 || exit 1
+  run K2 --workload K2 --steps 420 --warmup 42 || exit 1
+  run K4 --workload K4 --steps 420 --warmup 42 || exit 1
+  run K3 --workload K3 --steps 420 --warmup 42 || exit 1
+  run K5 --workload K5 --steps 420 --warmup 42 || exit 1
 }
 [ -z "$SKIP_REPS" ] && {
   for args in "2048 4096 f64" "2048 4096 f64 --ring" "1024 4096 f64" "1024 4096 f64 --ring" "512 4096 f64" "512 4096 f64 --ring" \

@@ -4,7 +4,7 @@ RCCL self ring, optionally with the K5 filament array) primed once, then REPS ti
 STEPS iterations each; prints one JSON line with the ms/iteration of every repetition and the
 spread (max/min - 1).
 
-usage: scripts/ring_reps.py NX NY PRECISION [--ring] [--k5 OFFSET] [--reps 7] [--steps 300] [--same-phase]
+usage: scripts/ring_reps.py NX NY PRECISION [--ring] [--k5 OFFSET] [--reps 7] [--steps 420] [--same-phase]
 
 --same-phase (with --k5): every timed region gets the points of the same STEPS iterations of the
 beat (the lattice state goes on), so the regions do the same work; without it the regions follow
@@ -30,7 +30,7 @@ def main():
     p.add_argument("--ring", action="store_true")
     p.add_argument("--k5", type=float, default=None, help="K5 filaments (8 per 1024 columns) at this offset")
     p.add_argument("--reps", type=int, default=7)
-    p.add_argument("--steps", type=int, default=300)
+    p.add_argument("--steps", type=int, default=420)
     p.add_argument("--same-phase", action="store_true")
     a = p.parse_args()
     import cuda_iblb_11_amd as P

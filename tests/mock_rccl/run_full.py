@@ -36,7 +36,7 @@ NX, NY = 8192, 2048
 
 def main():
     n, kind = int(sys.argv[1]), sys.argv[2]
-    K = int(os.environ.get("IBLB_SWEEP_DEPTH", "6"))  # the library's deep-sweep depth
+    K = int(os.environ.get("IBLB_SWEEP_DEPTH", "7"))  # the library's deep-sweep depth
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 1 + 4 * K
     ib = kind == "K5"
     prec = "f32" if ib else "f64"

@@ -20,9 +20,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 TOL64, TOL32, TIGHT = 1e-6, 1e-4, 1e-9
-# the library's deep-sweep depth (IBLB_SWEEP_DEPTH, default 6): the step counts below are built from
+# the library's deep-sweep depth (IBLB_SWEEP_DEPTH, default 7): the step counts below are built from
 # it, so that "boot + two deep launches" is 1 + 2K iterations whatever K is
-K = int(os.environ.get("IBLB_SWEEP_DEPTH", "6"))
+K = int(os.environ.get("IBLB_SWEEP_DEPTH", "7"))
 CHUNKS = [1, 2 * K + 2, K, 3, 3 * K]  # boot, two cycles + 2, one cycle, 3 one-step, three cycles
 
 

@@ -17,9 +17,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 TOL64, TOL32, TIGHT = 1e-6, 1e-4, 1e-9
-# the library's deep-sweep depth (IBLB_SWEEP_DEPTH, default 6): the band tests' step counts are built
+# the library's deep-sweep depth (IBLB_SWEEP_DEPTH, default 7): the band tests' step counts are built
 # from it (a chunk of n >= K iterations runs n // K band cycles)
-K = int(os.environ.get("IBLB_SWEEP_DEPTH", "6"))
+K = int(os.environ.get("IBLB_SWEEP_DEPTH", "7"))
 
 
 def rel(a, b):
@@ -583,7 +583,7 @@ def test_rccl_self_ring_bulk(gpu, monkeypatch, precision, overlap, depth):
     ring.close()
 
 
-@pytest.mark.parametrize("depth", [3, 4, 5, 6])
+@pytest.mark.parametrize("depth", [3, 4, 5, 6, 7])
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
     """K = 3 or 4 iterations per launch (IBLB_SWEEP_DEPTH=K, lone slab: K-1 register windows,
