@@ -309,9 +309,9 @@ def main():
             go = bool(flag.item() > 0)
         if not go:
             break
-        drv.run(50)
+        drv.run(42)  # whole deep cycles at every depth 3 ... 7
         lat.synchronize()
-        prime_steps += 50
+        prime_steps += 42
     prime_s = time.perf_counter() - tp
     # the points of the warmup and the timed steps given ahead in one schedule: nothing of the
     # timed iterations (not even the force owed at its start) is evaluated before the timer

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Evidence of the current tree (run from the repo root through gpurun; TAG names the run):
 #   1. the whole -m gpu suite, smoke, the driver's default bench line (with the CPU baseline);
-#   2. rocprofv3 kernel-trace stats of the same bench command (the dominant kernel's mean duration);
+#   2. rocprofv3 kernel-trace stats of the default bench command (the dominant kernel's mean duration);
 #   3. HBM traffic (FETCH_SIZE and WRITE_SIZE in separate --pmc passes) and SQ VALU passes of the
 #      deep f64 / f32 launches -> profiles/pmc_traffic.json / pmc_valu.json (scripts/pmc_*.py);
 #   4. every BASELINE config at N = 1 (M at the driver's 20 steps and at 420, M f32, K2, K3, K4, K5);
@@ -30,7 +30,7 @@ mkdir -p "$OUT"
 B="python3 bench.py --no-cpu-baseline"
 [ -z "$SKIP_PMC" ] && {
   timeout -k 10 -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace \
-    -- $B --steps 210 --warmup 21 --prime-seconds 0.5 > "$OUT/trace_bench.json" 2> "$OUT/trace.err" || { tail -20 "$OUT/trace.err"; exit 1; }
+    -- $B > "$OUT/trace_bench.json" 2> "$OUT/trace.err" || { tail -20 "$OUT/trace.err"; exit 1; }
   find "$OUT/trace" -name "*kernel_stats.csv" -exec head -4 {} \;
   # the depth-7 launches only (the default; a call's K-1 launches carry the same bytes): 70 steps =
   # ten of them, the kernel named with its template arguments (f64 variant 35 -> mode 273, f32 11 -> 81)

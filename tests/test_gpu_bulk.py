@@ -347,7 +347,7 @@ def test_rccl_self_ring_ib_band_cycle(gpu, monkeypatch, precision, where):
     ring.attach_rccl(gpu.rccl_unique_id(), 1, 0)
     ring.set_profiling(True)
     t = 0
-    for n in (1, 12, 7, 10):
+    for n in (1, 2 * K, K, K + 3):
         for lat in (ref, ring):
             lat.set_lagrangian_steps(*_schedule(pts, t, n))
             lat.step(n)

@@ -418,6 +418,11 @@ def test_cilia_band_cycle(gpu, oracle, precision, monkeypatch):
     1024 x 192, 4K + 3 iterations in chunks (1, 4K, 2): boot, four band cycles, one-step remainders with
     the kinematics launched per iteration again; against the oracle fed by the restated kinematics
     and against the one-step path (IBLB_IB_BAND=0)."""
+    # depth 5 here: at 7 the f32 run declined every band plan (measured: no deep launch).  The plan
+    # rule (ctx_band.hip: trapezoids over half the lattice's updates -> one-step iterations) counts
+    # whole one-step row chunks, 256 rows in f32: all 192 rows of this lattice in every column-level.
+    monkeypatch.setenv("IBLB_SWEEP_DEPTH", "5")
+    K = 5
     from cuda_iblb_11_amd import workloads as W
     c_num, c_space, T = 8, 128.0, 100000
     nx, ny, steps = int(c_num * c_space), 192, 4 * K + 3
@@ -838,7 +843,7 @@ def _ulps(a, b):
 def test_ib_band_many_points(gpu, oracle, precision, monkeypatch):
     """150 points in three filaments (two merged into one patch), chunked calls with readers
     between them: the band cycle against the one-step path (IBLB_IB_BAND=0) and the oracle.
-    vs the oracle the f64 bound is 1e-8, not the 1e-10 of the two-filament tests: the reference
+    vs the oracle the f64 bound is 5e-8, not the 1e-10 of the two-filament tests: the reference
     accumulates F_s in float (ImmersedBoundary.cu:124-125), so the 1e-16 rounding differences of
     the collide flip some F_s by one float ulp (6e-8 relative) — checked here ulp by ulp, and
     reproduced by the oracle against itself in tests/test_oracle.py::test_fs_float_ulp_flips."""
@@ -858,8 +863,8 @@ def test_ib_band_many_points(gpu, oracle, precision, monkeypatch):
             d = _ulps(runs[band][2], sim.F_s)
             assert d.max() <= 64 and rel(runs[band][2], sim.F_s) <= 1e-6, (band, int(d.max()))
         lat.close()
-    for e in errs.values():
-        assert max(e["rho"], e["ux"], e["uy"]) <= (1e-8 if precision == "f64" else TOL32), errs
+    for e in errs.values():  # (the flips' effect grows with the run: 1.3e-8 after 38 iterations)
+        assert max(e["rho"], e["ux"], e["uy"]) <= (5e-8 if precision == "f64" else TOL32), errs
     assert runs[0][4]["sweepk_launches"] == 0 and runs[1][4]["sweepk_launches"] >= 5
     (r1, u1), (r0, u0) = runs[1][0], runs[0][0]
     tol = (1e-13, 1e-12) if precision == "f64" else (1e-6, 1e-5)
