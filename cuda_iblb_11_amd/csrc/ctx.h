@@ -195,6 +195,7 @@ struct iblb_ctx {
               sweepk_cells = 0;
     long long band_cycles = 0, band_merged_cycles = 0, band_par_cycles = 0;  // IB band cycles run (counted without events too)
     long long deep_launches = 0, deep_iterations = 0;  // deep launches and the iterations they advanced (no events needed)
+    bool band_own_build = false;  // the band cycle's deep sweep in the configured (not the chain-friendly) build
     struct EvRec { int kind; size_t idx; long long cells; };
     std::vector<EvRec> ev_kind;
     std::string err;

@@ -78,7 +78,20 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
     const double share = (double)band_cols / (double)std::max(1LL, band_cols + (long long)c->sweep_depth * deep_cols);
     long want = (share > 0.05 ? 2 : 1) * per_xcd;
     const double deep_us = (double)c->sweep_depth * deep_cols * c->ny / (is_f64(c) ? 130e3 : 190e3);
-    if (!slab && deep_us >= 1.5 * 2 * c->sweep_depth * 8.0) want = -2;
+    // f32 at depth >= 7: the chain on one XCD's worth of CUs of its own and the deep sweep in its own
+    // build (the packed wall split) on the rest: K5 242.5-243.2k MLUPS against 221.4-221.9k for both
+    // streams unmasked beside the scalar build, 231.5-232.7k unmasked beside the packed split; the
+    // chain on 16 / 64 CUs 178k / 212k (profiles/r04/k5var).  (At depth 5 the same arrangement lost:
+    // 196-207k vs 221-227k, profiles/r04/k5deep.)  f64: both unmasked (K3 136k vs 128k masked).
+    bool own_build = false;
+    if (!slab && deep_us >= 1.5 * 2 * c->sweep_depth * 8.0) {
+        if (!is_f64(c) && c->sweep_depth >= 7) {
+            want = per_xcd;
+            own_build = true;
+        } else {
+            want = -2;
+        }
+    }
     std::vector<uint32_t> base((size_t)(c->ncu + 31) / 32, 0u);
     int avail = 0;
     for (int i = 0; i < c->ncu; ++i)
@@ -91,6 +104,7 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
     want = env_long("IBLB_BAND_CUS", want);
     if (want == -2 && slab) want = per_xcd;  // a group slab's comm stream owns the reserved CUs
     if (want >= avail) want = 0;
+    c->band_own_build = own_build && want == per_xcd;
     if (want == c->band_reserve || (c->band_sticky && c->band_st)) return IBLB_OK;
     if ((rc_ = band_join(c))) return rc_;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -383,9 +397,11 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     d.vs = slab ? c->slab_vs : c->deep_vs;
     // f32: the two-wave scalar-collide build: the three-wave f32 wall split leaves the chain's kernels
     // no room beside the deep sweep (K5 197.6k vs 193.9k MLUPS with it, profiles/r03sp), and the
-    // packed builds (two waves of 191 / 228 VGPRs) measured 209k / 202k vs 215k (profiles/r04/pack).
+    // packed builds (two waves of 191 / 228 VGPRs) measured 209k / 202k vs 215k (profiles/r04/pack)
+    // -- except where the chain has CUs of its own beside a long deep sweep (band_own_build, depth
+    // >= 7: K5 243k vs 222k MLUPS, profiles/r04/k5var).
     // f64: the configured variant (its wall split keeps one wave per SIMD; not with PAR's skip boxes)
-    d.variant = sizeof(T) == 8 ? c->deep_variant : c->deep_variant & 1;
+    d.variant = sizeof(T) == 8 || c->band_own_build ? c->deep_variant : c->deep_variant & 1;
     d.cus = c->ncu ? (slab ? c->ncu - c->reserved_cus : c->ncu) - std::max(0, c->band_reserve) : 0;
     if (c->band_flux >= 0) {
         d.fskip0 = c->band_fy0;
@@ -700,6 +716,7 @@ int band_release(iblb_ctx* c) {
     c->band_pin_cap = 0;
     c->band_pin_i = 0;
     c->band_reserve = 0;
+    c->band_own_build = false;
     c->band_valid = false;
     c->band_b.clear();
     c->band_d = c->band_x = 0;
