@@ -291,14 +291,16 @@ def test_errors_are_loud(gpu):
                           (2, True, "f64", 1, 0, 5), (4, True, "f64", 1, 0, 5), (2, False, "f32", 1, 0, 5),
                           (2, False, "f64", 1, 1, 5), (3, False, "f64", 1, 1, 5), (3, False, "f64", 0, 1, 5),
                           (4, False, "f32", 1, 1, 5), (2, False, "f64", 1, 1, 2), (3, False, "f32", 1, 1, 2),
-                          (3, False, "f64", 1, 1, 3), (4, False, "f64", 1, 1, 6)])
+                          (3, False, "f64", 1, 1, 3), (4, False, "f64", 1, 1, 6), (3, False, "f64", 1, 1, 7),
+                          (2, False, "f32", 1, 1, 7)])
 def test_rccl_slab_path_threads(gpu, n, with_ib, precision, overlap, bulk, depth, nx=48):
     """The RCCL transport of iblb_ctx.hip (attach, halo send/recv pairing, node-value and
     flux all-reduces, collective readers) driven with N ranks as threads on the one GPU via
     the mock-RCCL test build (RCCL itself refuses two ranks on one device).  Without IB the
     decomposed run must be bit-identical to one slab; bulk: multi-step calls, i.e. the
-    multi-iteration sweeps (depth 2: the 2-step halo; 3-6: the deep halo) with the boundary
-    sweeps on the comm stream."""
+    multi-iteration sweeps (depth 2: the 2-step halo; 3-7: the deep halo; a call of 13 iterations
+    at depth 5 or 7 mixes depths K - 1 and K, ctx_step.hip:deep_depth) with the boundary sweeps on
+    the comm stream."""
     import json
     import os
     import subprocess
