@@ -756,7 +756,8 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
 template <int K, int VS>
 constexpr int ghost_lanes() { return (K - 1 + VS - 1) / VS; }
 
-// Wall split (MODE_SPLIT, balanced sweeps only).  The rows split into a bottom wall chunk [0, OWN1),
+// Wall split (MODE_SPLIT; balanced sweeps, or fixed ones such as a slab's boundary sweeps, round 4).
+// The rows split into a bottom wall chunk [0, OWN1),
 // the inner rows [OWN1, a.wall_top) in chunks of OWN*VS and a top wall chunk [a.wall_top, ny), where
 // OWN1 = 64 - 2(K-1) rows is one wave of one cell per lane.  The inner chunks are walked by the
 // kernel's VS-cell walk without wall code (a.nsweep sweeps each); the two wall chunks by a one-cell
@@ -907,8 +908,10 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
             b.nsweep = (int)std::min(ns, n);
             waves = (long)b.nsweep * b.nch;
         }
+    } else if (MODE & MODE_SPLIT) {  // fixed sweeps (a slab's boundary sweeps): the wall chunks too
+        b.nsweep_w = b.nsweep;
+        waves = (long)b.nsweep * b.wall_ch0 + 2L * b.nsweep_w;
     } else {
-        if (MODE & MODE_SPLIT) return hipErrorInvalidValue;  // the split needs balanced sweeps
         waves = (long)b.nsweep * b.nch;
     }
     const unsigned blocks = (unsigned)((waves + 3) / 4);
@@ -935,7 +938,7 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
         // row (two-cell lanes of the inner chunks never straddle it) holding the last OWN1 or fewer rows
         constexpr int OWN1 = 64 - 2 * ghost_lanes<K, 1>();
         const int top = (a.L.ny - OWN1 + 1) & ~1;
-        if ((a.variant & 2) && (VS == 2 || (a.variant & 64)) && a.col_step <= 0 && a.nskip == 0 && top > OWN1) {
+        if ((a.variant & 2) && (VS == 2 || (a.variant & 64)) && a.nskip == 0 && top > OWN1) {
             b.wall_top = top;
             b.wall_ch0 = (top - OWN1 + rows_per_wave - 1) / rows_per_wave;
             // bit 3: the inner chunks packed, two waves per SIMD (the packed inner walk needs 191 VGPRs;
