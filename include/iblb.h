@@ -140,12 +140,13 @@ typedef struct iblb_timing {
     long long sweep_launches;  /* timed two-iteration launches                           */
     double    sweep_ms;        /* their summed duration                                  */
     long long sweep_cells;     /* cells they covered (lattice updates = 2 x sweep_cells) */
-    /* deep launches (lone slab, IBLB_SWEEP_DEPTH = K >= 3): state read and written once for K
+    /* deep launches (IBLB_SWEEP_DEPTH = K >= 3): state read and written once for K (or K-1)
      * iterations */
     long long sweepk_launches;
     double    sweepk_ms;
-    long long sweepk_cells;    /* lattice updates = sweepk_depth x sweepk_cells */
-    long long sweepk_depth;    /* K */
+    long long sweepk_cells;    /* cells they covered; lattice updates = sweepk_cells x the launches'
+                                * depths (deep_iterations / deep_launches on average) */
+    long long sweepk_depth;    /* K, the configured depth */
     /* IB band cycles run (ctx_band.hip), and how many of them ran the merged chain; counted
      * whether or not profiling events are on */
     long long band_cycles;
