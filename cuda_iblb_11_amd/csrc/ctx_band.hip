@@ -78,6 +78,13 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
     const double share = (double)band_cols / (double)std::max(1LL, band_cols + (long long)c->sweep_depth * deep_cols);
     long want = (share > 0.05 ? 2 : 1) * per_xcd;
     const double deep_us = (double)c->sweep_depth * deep_cols * c->ny / (is_f64(c) ? 130e3 : 190e3);
+    // a group slab's merged chain at depth >= 7 (its short deep sweep, plan_bands_t): two XCDs' worth.
+    // Its launches (~640 waves on the K5-width slab) take two rounds on 32 CUs at four waves per SIMD;
+    // self ring, five alternations (profiles/r04/cus3264): 2048 x 2048 edge 0.0320 vs 0.0342 ms per
+    // iteration, 1024 x 2048 edge 0.0242 vs 0.0250, mid-slab equal; the chained chain beside the long
+    // deep sweep of a 4096-column slab keeps one (0.0495 vs 0.0546 with two, profiles/r04/slabcus)
+    const bool merged = c->band_merge == 2 || (c->band_merge == 1 && deep_us < 1.5 * 2 * c->sweep_depth * 8.0);
+    if (slab && merged && c->sweep_depth >= 7) want = 2 * per_xcd;
     // f32 at depth >= 7: the chain on one XCD's worth of CUs of its own and the deep sweep in its own
     // build (the packed wall split) on the rest: K5 242.5-243.2k MLUPS against 221.4-221.9k for both
     // streams unmasked beside the scalar build, 231.5-232.7k unmasked beside the packed split; the
