@@ -1,6 +1,7 @@
 """The drop-in boundary on CPU: libiblb.so loads, exports every function include/iblb.h
 declares, and refuses to run without a HIP device (no CPU fallback)."""
 import ctypes as C
+import os
 import subprocess
 
 import numpy as np
@@ -84,3 +85,30 @@ def test_split_helpers_roundtrip():
     fp = [P.split_populations(f, nx, ny, xb, xc) for xb, xc in P.plan_slabs(nx, 2)]
     back = np.concatenate([p.reshape(ny, -1, 9) for p in fp], axis=1).ravel()
     assert np.array_equal(back, f)
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """The Python mirror's ctypes structs (cuda_iblb_11_amd/_lib.py) against the C header: size and
+    every field's offset of iblb_config, iblb_timing and iblb_cilia, from a C program compiled
+    with gcc against include/iblb.h (no device needed)."""
+    import shutil
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    structs = {"iblb_config": L.Config, "iblb_timing": L.Timing, "iblb_cilia": L.Cilia}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "iblb.h"', 'int main(void) {']
+    for cname, py in structs.items():
+        lines.append(f'    printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'    printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines += ['    return 0;', '}']
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(repo, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {(ln.split()[0], ln.split()[1]): int(ln.split()[2]) for ln in out if ln.strip()}
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == C.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
