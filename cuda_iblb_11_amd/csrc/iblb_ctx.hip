@@ -339,10 +339,12 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->sweep_depth = (int)std::min(7L, std::max(2L, env_long("IBLB_SWEEP_DEPTH", 7)));
     c->deep_w = (int)env_long("IBLB_DEEP_W", f64 ? 96 : 64);
     c->deep_vs = (int)env_long("IBLB_DEEP_VS", 2);
-    // f32: the wall split (variant bit 1) with the packed collide (bit 3), profiles/r04/pack; f64: the
-    // wall split with the level-1 preshift (bits 1, 5: M f64 0.480 vs 0.521 ms per launch,
+    // f32: the wall split (variant bit 1) with the packed collide (bit 3), profiles/r04/pack, and on
+    // one-cell group slabs the split with the preshift (bits 5, 6: 107 = 11 | 32 | 64; self ring
+    // 512 x 4096 0.01158 vs 0.01242 ms/iteration, 2048 x 2048 0.0187 vs 0.0210, profiles/r04/depth);
+    // f64: the wall split with the level-1 preshift (bits 1, 5: M f64 0.480 vs 0.521 ms per launch,
     // profiles/r04/split64)
-    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 35 : 11);
+    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 35 : 107);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_merge = (int)env_long("IBLB_BAND_MERGE", 1);
