@@ -408,7 +408,9 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     // -- except where the chain has CUs of its own beside a long deep sweep (band_own_build, depth
     // >= 7: K5 243k vs 222k MLUPS, profiles/r04/k5var).
     // f64: the configured variant (its wall split keeps one wave per SIMD; not with PAR's skip boxes)
-    d.variant = sizeof(T) == 8 || c->band_own_build ? c->deep_variant : c->deep_variant & 1;
+    // without the LDS window (bit 7): its 144 KB per workgroup would keep the chain's LDS-using
+    // kernels off the deep sweep's CUs (K3 136.0 / 137.1k vs 137.5 / 140.9k MLUPS, profiles/r04/ldswin)
+    d.variant = sizeof(T) == 8 ? c->deep_variant & ~128 : c->band_own_build ? c->deep_variant : c->deep_variant & 1;
     d.cus = c->ncu ? (slab ? c->ncu - c->reserved_cus : c->ncu) - std::max(0, c->band_reserve) : 0;
     if (c->band_flux >= 0) {
         d.fskip0 = c->band_fy0;
@@ -636,7 +638,7 @@ static int band_step(iblb_ctx* c) {
         if (before_deep) HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_deep, 0));
         Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
         b.vs = c->slab_vs;
-        b.variant = c->deep_variant;
+        b.variant = c->deep_variant & ~128;  // beside the chain: no LDS window (above)
         if (c->band_flux >= 0) {
             b.fskip0 = c->band_fy0;
             b.fskip1 = c->band_fy1;

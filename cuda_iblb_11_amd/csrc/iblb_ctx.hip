@@ -343,8 +343,9 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     // one-cell group slabs the split with the preshift (bits 5, 6: 107 = 11 | 32 | 64; self ring
     // 512 x 4096 0.01158 vs 0.01242 ms/iteration, 2048 x 2048 0.0187 vs 0.0210, profiles/r04/depth);
     // f64: the wall split with the level-1 preshift (bits 1, 5: M f64 0.480 vs 0.521 ms per launch,
-    // profiles/r04/split64)
-    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 35 : 107);
+    // profiles/r04/split64) and the LDS window (bit 7: 163 = 35 | 128; M f64 0.621 vs 0.633 ms per
+    // depth-7 launch, 512-column self ring 0.0159 vs 0.0163 ms/iteration, profiles/r04/ldswin)
+    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 163 : 107);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_merge = (int)env_long("IBLB_BAND_MERGE", 1);

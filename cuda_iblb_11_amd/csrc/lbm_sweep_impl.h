@@ -39,7 +39,7 @@ namespace iblb {
 
 // sweep only (MODE bits 1, 2 as in lbm_vec.h): no software prefetch of the next column (two-step
 // sweeps); the deep sweep's wall split (sweepk_kernel)
-enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16, MODE_PACK = 64, MODE_SKIP = 128, MODE_PRESHIFT = 256 };
+enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16, MODE_PACK = 64, MODE_SKIP = 128, MODE_PRESHIFT = 256, MODE_LDSWIN = 512 };
 
 namespace {
 
@@ -653,12 +653,24 @@ __device__ __forceinline__ bool skip_rows(const Sweep2Args<T>& a, int c, int r0,
 // level K, counted in the flux) all come later.  (Running every level from iteration 0 instead,
 // on not-yet-valid windows, lets the compiler hoist the collide constants out of the walk and
 // needs more registers than the wave has: measured 40 % slower, profiles/r02c_*.)
-template <typename T, int VS, int MODE, int K, bool SLAB, bool REV>
+// LDS window (MODE_LDSWIN, f64 inner chunks of the wall split, two cells per lane): the three
+// populations of a level's column that move along the walk (c_x = DX) are needed two iterations after
+// they are made; they wait in LDS (two slots by iteration parity, 16 B per lane and population, 144 KB
+// per workgroup at K = 7) instead of VGPRs, so the register window keeps only the three c_x = 0
+// populations of the middle column: 256 VGPRs + 4 AGPRs instead of 256 + 142 at K = 7, no AGPR moves
+// in the walk (profiles/r04/ldswin).
+template <typename T, int VS, int MODE, bool WL>
+constexpr bool lds_window() { return (MODE & MODE_LDSWIN) && sizeof(T) == 8 && VS == 2 && !WL; }
+template <int K, int VS>
+constexpr int lds_window_wave() { return 2 * (K - 1) * 3 * 64 * VS; }  // elements per wave
+
+template <typename T, int VS, int MODE, int K, bool SLAB, bool REV, bool LW>
 __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int nl1, int x0, int xa, int xb, int row0,
                                             unsigned off, int lane, int r0, int et, bool owner, bool bot, bool top,
                                             bool walls, T (&WA)[K - 1][9][VS], T (&WB)[K - 1][9][VS],
                                             Raw<T, VS>& cur, double& q, const BufOfs& bo,
-                                            __amdgpu_buffer_rsrc_t (&rc)[3], bool fin, int fi, int fown, SkipState& sp) {
+                                            __amdgpu_buffer_rsrc_t (&rc)[3], bool fin, int fi, int fown, SkipState& sp,
+                                            T* lw) {
     constexpr int DX = REV ? -1 : 1;
     const int x = x0 + i * DX;
     T N[9][VS];
@@ -683,6 +695,20 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
         const bool flux = fin && i == fi + l - 1;
         T out[9][VS];
         const bool made = i >= 2 * (l - 1);
+        typedef typename VT<T, VS>::type vec;
+        vec* ls = nullptr;
+        if constexpr (LW) {  // slot of parity i: the column made two iterations ago, then this one's
+            ls = (vec*)(lw + ((i & 1) * (K - 1) + (l - 2)) * 3 * 64 * VS);
+            int p = 0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k)
+                if (cx(k) == DX) {
+                    const vec v = ls[p * 64];
+#pragma unroll
+                    for (int e = 0; e < VS; ++e) WA[l - 2][k][e] = v[e];
+                    ++p;
+                }
+        }
         if (made) level_from_window<T, VS, DX, MODE>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, fown, q, out);
         // level K's columns of the made steps are exactly the sweep's outputs [xa, xb)
         bool keep = owner;
@@ -693,8 +719,26 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
 #pragma unroll
             for (int k = 0; k < 9; ++k) st_rows_buf<T, VS, MODE>(rd, bo.lane, (unsigned)k * bo.plane, out[k]);
         }
-        copy_col<T, VS>(WA[l - 2], WB[l - 2]);
-        copy_col<T, VS>(WB[l - 2], N);
+        if constexpr (LW) {
+            int p = 0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k)
+                if (cx(k) == DX) {
+                    vec v;
+#pragma unroll
+                    for (int e = 0; e < VS; ++e) v[e] = N[k][e];
+                    ls[p * 64] = v;
+                    ++p;
+                }
+#pragma unroll
+            for (int k = 0; k < 9; ++k)
+                if (cx(k) == 0)
+#pragma unroll
+                    for (int e = 0; e < VS; ++e) WB[l - 2][k][e] = N[k][e];
+        } else {
+            copy_col<T, VS>(WA[l - 2], WB[l - 2]);
+            copy_col<T, VS>(WB[l - 2], N);
+        }
         if (l < K && made) copy_col<T, VS>(N, out);
     }
 }
@@ -705,7 +749,7 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
 // wall code and keep no wall planes of the windows live)
 template <typename T, int VS, int MODE, int K, bool SLAB, bool REV, bool WL>
 __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
-                                              int lane, int r0, int et, bool owner, bool bot_, bool top_) {
+                                              int lane, int r0, int et, bool owner, bool bot_, bool top_, T* lw) {
     const bool walls = WL, bot = WL && bot_, top = WL && top_;
     const int x0 = REV ? xb + K - 2 : xa - (K - 1);
     const int nl1 = xb - xa + 2 * (K - 1);  // level-1 columns xa-(K-1) .. xb+(K-2)
@@ -748,8 +792,9 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
         skip_load<T, VS, REV>(a, r0, sp);
     }
     for (int i = 0; i < nl1; ++i)
-        sweepk_iter<T, VS, MODE, K, SLAB, REV>(a, i, nl1, x0, xa, xb, row0, off, lane, r0, et, owner, bot, top, walls, WA,
-                                               WB, cur, q, bo, rc, fin, fi, fown, sp);
+        sweepk_iter<T, VS, MODE, K, SLAB, REV, lds_window<T, VS, MODE, WL>()>(a, i, nl1, x0, xa, xb, row0, off, lane, r0, et,
+                                                                        owner, bot, top, walls, WA, WB, cur, q, bo, rc,
+                                                                        fin, fi, fown, sp, lw);
     return q;
 }
 
@@ -789,6 +834,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     constexpr int OWN = 64 - 2 * G;  // owned lanes per wave
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    T* lw = nullptr;
+    if constexpr (lds_window<T, VS, MODE, false>()) {
+        __shared__ __attribute__((aligned(16))) T lwin[4 * lds_window_wave<K, VS>()];
+        lw = lwin + wv * lds_window_wave<K, VS>() + lane * VS;
+    }
     int sw, ch, nsw = a.nsweep;
     bool wall = false;
     if (MODE & MODE_SPLIT) {
@@ -818,8 +868,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const unsigned off = (unsigned)(lane * (int)sizeof(T));
         const int et = a.L.ny - 1 - r0;
         const bool owner = lane >= G1 && lane < 64 - G1 && r0 < a.L.ny && (ch == 1 || r0 < OWN1);
-        q = rev ? sweepk_walk<T, 1, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0)
-                : sweepk_walk<T, 1, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0);
+        q = rev ? sweepk_walk<T, 1, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0, lw)
+                : sweepk_walk<T, 1, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0, lw);
     } else if (MODE & MODE_SPLIT) {  // an inner chunk: no wall row within reach of its own rows
         constexpr int OWN1 = 64 - 2 * ghost_lanes<K, 1>();
         const int cs = OWN1 + ch * (OWN * VS);
@@ -828,8 +878,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
         const int et = a.L.ny - 1 - r0;
         const bool owner = lane >= G && lane < 64 - G && r0 < a.wall_top;
-        q = rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false)
-                : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false);
+        q = rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw)
+                : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw);
     } else {
         const int cs = ch * (OWN * VS);
         const int row0 = cs - G * VS;
@@ -841,10 +891,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const bool top = et >= 0 && et < VS;
         // wave-uniform: does the wave hold a wall row (y = 0 or Y-1, ghost lanes included)?
         const bool walls = row0 <= 0 || row0 + 64 * VS >= a.L.ny;
-        q = walls ? (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
-                         : sweepk_walk<T, VS, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top))
-                  : (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top)
-                         : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top));
+        q = walls ? (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top, lw)
+                         : sweepk_walk<T, VS, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top, lw))
+                  : (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top, lw)
+                         : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top, lw));
     }
     if (a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb) {
         const double qs = wave_sum(q);
@@ -947,6 +997,11 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
             if constexpr (sizeof(T) == 4 && VS == 2)
                 if (a.variant & 8)
                     return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PACK, K, SLAB, 2>(b, s, stop, start);
+            // bit 7 (f64, two cells per lane, with bit 5): the LDS window of the inner chunks
+            if constexpr (sizeof(T) == 8 && VS == 2)
+                if ((a.variant & 160) == 160)
+                    return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PRESHIFT | MODE_LDSWIN, K, SLAB, WPE>(b, s, stop,
+                                                                                                           start);
             if (a.variant & 32)
                 return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PRESHIFT, K, SLAB, WPE>(b, s, stop, start);
             if (a.variant & 1) return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT, K, SLAB, WPE>(b, s, stop, start);

@@ -9,7 +9,7 @@ out=cuda_iblb_11_amd/lib/variants; tmp=cuda_iblb_11_amd/vbuild_$name  # csrc dep
 rm -rf $tmp; mkdir -p $out $tmp
 cp cuda_iblb_11_amd/csrc/*.h cuda_iblb_11_amd/csrc/*.hip $tmp/
 cp $dir/* $tmp/ 2>/dev/null || true
-rebuild="lbm_sweep lbm_sweepk3 lbm_sweepk4 lbm_sweepk5 lbm_sweepk6 $(cd $dir && ls *.hip 2>/dev/null | sed 's/\.hip$//')"
+rebuild="lbm_sweep lbm_sweepk3 lbm_sweepk4 lbm_sweepk5 lbm_sweepk6 lbm_sweepk7 $(cd $dir && ls *.hip 2>/dev/null | sed 's/\.hip$//')"
 objs=""
 for f in $(cd cuda_iblb_11_amd/csrc && ls *.hip | sed 's/\.hip$//'); do
   if echo " $rebuild " | grep -q " $f "; then

@@ -33,9 +33,9 @@ B="python3 bench.py --no-cpu-baseline"
     -- $B > "$OUT/trace_bench.json" 2> "$OUT/trace.err" || { tail -20 "$OUT/trace.err"; exit 1; }
   find "$OUT/trace" -name "*kernel_stats.csv" -exec head -4 {} \;
   # the depth-7 launches only (the default; a call's K-1 launches carry the same bytes): 70 steps =
-  # ten of them, the kernel named with its template arguments (f64 variant 35 -> mode 273, f32 11 -> 81)
+  # ten of them, the kernel named with its template arguments (f64 variant 163 -> mode 785, f32 11 -> 81)
   for prec in f64 f32; do
-    if [ $prec = f64 ]; then kn="sweepk_kernel<double, 2, 273, 7,"; else kn="sweepk_kernel<float, 2, 81, 7,"; fi
+    if [ $prec = f64 ]; then kn="sweepk_kernel<double, 2, 785, 7,"; else kn="sweepk_kernel<float, 2, 81, 7,"; fi
     for c in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 -s KILL 180 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${c}_$prec" -o pmc \
         -- $B --precision $prec --steps 70 --warmup 7 --prime-seconds 0.3 --no-profile-events > /dev/null 2> "$OUT/pmc_${c}_$prec.err" \

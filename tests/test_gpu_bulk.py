@@ -123,7 +123,7 @@ def test_m_bulk_f32(gpu, oracle, threads):
 
 
 def test_k1_1000_steps_bulk_f32(gpu, oracle, threads):
-    """f32 over the longest horizon: 128^2, 1000 iterations in one call (199 deep launches), within
+    """f32 over the longest horizon: 128^2, 1000 iterations in one call (~1000 / K deep launches), within
     the north star's 1e-4 on rho - 1, u_x, u_y (each normalised by its own max).  By then rho - 1
     has decayed to ~1e-5 while f32 rounding keeps adding ~1e-12 per cell and iteration; a plain
     numpy float32 restatement (tests/f32_model.py) lands at 1.5e-4 on rho - 1 and u_y.  The kernels'
