@@ -1,5 +1,6 @@
 # f64 deep sweep: the moving populations of the level windows in LDS (IBLB_LDSWIN=1 build via
 # IBLB_LIB: 260 instead of 398 VGPRs+AGPRs) vs the default, bit identity first, then alternated
+# (historical: the IBLB_LDSWIN compile switch became variant bit 7; scripts/r04_ldswin2.sh reruns the A/B)
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/r04lw
