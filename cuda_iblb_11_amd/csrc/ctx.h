@@ -186,6 +186,12 @@ struct iblb_ctx {
     long long deep_chain_t = -1;  // ... that ended at this t with this cur: ev_int follows its interior
     int deep_chain_cur = -1;
     bool overlap = true;          // IBLB_OVERLAP
+    // deep slab cycles: the interior's edge waves wait on a device word the comm stream's boundary
+    // sweeps signal (IBLB_EDGE_FLAG, default on) instead of the compute queue waiting for ev_bnd
+    bool edge_flag = true;
+    unsigned* sig = nullptr;      // device word: sequence number of the last boundary launch done
+    unsigned sig_n = 0;           // boundary launches signalled so far (the value of the last one)
+    unsigned* sig_err = nullptr;  // host-coherent word: an edge wave's bounded wait timed out
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -308,6 +314,7 @@ int ensure_force(iblb_ctx* c);
 int ib_ghost(iblb_ctx* c, const void* g, int gc, int clo, int chi, const float* s, const float* us, const int* eps,
              int part, hipStream_t st);
 int check_ready(iblb_ctx* c);
+int check_wait_err(iblb_ctx* c);  // after a synchronize: did an edge wave's wait time out?
 int prepare_read(iblb_ctx* c);
 int free_boot(iblb_ctx* c);
 int alloc_zero(iblb_ctx* c, void** p, size_t bytes);

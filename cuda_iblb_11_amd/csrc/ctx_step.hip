@@ -365,11 +365,22 @@ static int sweepk_step(iblb_ctx* c, int d) {
 // K may differ from the previous cycle's (deep_depth): the exchange waits for the previous interior
 // when it sends columns that interior wrote (comm_ready: K > bnd_w), and every ghost column read is
 // within gc = 3 sweep_depth.
+// Edge flag (round 5, IBLB_EDGE_FLAG=1 default): in a chain of cycles the compute stream no longer
+// waits for boundary(t-K) (a barrier packet that cost ~9 us between consecutive interiors although
+// it was satisfied long before, profiles/r04/bsplit).  Only the interior's first and last sweeps
+// depend on boundary(t-K) — they pull columns [0, K) / [ncol-K, ncol) it wrote and overwrite
+// columns [K, 2K) / [ncol-2K, ncol-K) it read — so those waves wait on a device word the comm
+// stream sets after boundary(t-K) (a signal kernel: launch_seq_signal), with a bounded poll
+// (lbm_sweep_impl.h:edge_wait); every other wave starts at once.  The interior is then launched as
+// a ghost-column build (it reads no ghost column: the same cells, addressed without the periodic
+// wrap).  Deadlock freedom with shared hardware queues: DESIGN.md §8 (the wait graph).
 template <typename T>
 static int deep_slab_step(iblb_ctx* c, int K) {
     const int W = std::max(1, c->deep_w);
     const bool ov = c->overlap;
-    int rc = join_comm(c);
+    const bool chained = ov && c->deep_chain && c->deep_chain_t == c->t && c->deep_chain_cur == c->cur;
+    const bool flag = chained && c->edge_flag && c->sig;
+    int rc = flag ? IBLB_OK : join_comm(c);
     if (rc) return rc;
     hipStream_t bs = ov ? c->comm_stream : c->stream;
     const int ni = c->ncol - 2 * K;  // interior [K, ncol-K): needs nothing from the halo
@@ -382,10 +393,17 @@ static int deep_slab_step(iblb_ctx* c, int K) {
         a.vs = c->slab_vs;
         a.cus = c->ncu - c->reserved_cus;  // the compute stream's CU mask
         a.variant = c->deep_variant;
+        if (flag) {  // the value boundary(t-K) signalled; waves with outputs in [K, 2K) or [ncol-2K, ncol-K)
+            a.wait_seq = c->sig;
+            a.wait_val = c->sig_n;
+            a.wait_lo = 2 * K;
+            a.wait_hi = c->ncol - 2 * K;
+            a.wait_err = c->sig_err;
+        }
         size_t ev = 0;
         int r = ev_begin(c, &ev, c->stream);
         if (r) return r;
-        HIP_TRY(c, launch_sweepk<T>(a, K, false, c->stream, stop));
+        HIP_TRY(c, launch_sweepk<T>(a, K, flag, c->stream, stop));
         return ev_end(c, ev, EV_SWEEPK, (long long)ni * c->ny, c->stream);
     };
     auto boundary = [&](hipEvent_t stop) -> int {
@@ -402,13 +420,13 @@ static int deep_slab_step(iblb_ctx* c, int K) {
     } else {
         // prev: the compute stream's work before interior(t) (interior(t-K) when chained)
         hipEvent_t prev = c->ev_int, next = c->ev_int2;
-        if (!(c->deep_chain && c->deep_chain_t == c->t && c->deep_chain_cur == c->cur))
-            HIP_TRY(c, hipEventRecord(prev, c->stream));
+        if (!chained) HIP_TRY(c, hipEventRecord(prev, c->stream));
         if ((rc = interior(next))) return rc;
         if ((rc = comm_ready(c, K))) return rc;  // (waits for c->ev_int = prev)
         if ((rc = exchange(c, bs, K))) return rc;
         HIP_TRY(c, hipStreamWaitEvent(bs, prev, 0));
         if ((rc = boundary(c->ev_bnd))) return rc;
+        if (c->edge_flag && c->sig) HIP_TRY(c, launch_seq_signal(c->sig, ++c->sig_n, bs));
         c->ev_int = next;
         c->ev_int2 = prev;
         c->bnd_w = K;
@@ -420,6 +438,17 @@ static int deep_slab_step(iblb_ctx* c, int K) {
     c->deep_chain_t = c->t;
     c->deep_chain_cur = c->cur;
     return IBLB_OK;
+}
+
+// An edge wave's bounded wait (deep_slab_step) that timed out leaves wrong populations behind: the
+// call that ran it fails (the flag is read after the streams are synchronised).
+int check_wait_err(iblb_ctx* c) {
+    if (!c->sig_err || __atomic_load_n(c->sig_err, __ATOMIC_ACQUIRE) == 0) return IBLB_OK;
+    __atomic_store_n(c->sig_err, 0u, __ATOMIC_RELEASE);
+    c->deep_chain = false;
+    return fail(c, IBLB_ERR_COMM,
+                "a slab interior's edge wave timed out waiting for the boundary sweeps of the previous cycle "
+                "(comm stream stalled); the state is invalid");
 }
 
 int check_ready(iblb_ctx* c) {
@@ -570,7 +599,7 @@ int iblb_step(iblb_ctx* c, int nsteps) {
     }
     if ((rc = band_join(c))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return IBLB_OK;
+    return check_wait_err(c);
 }
 
 // ---- local groups -------------------------------------------------------------------------------
@@ -792,6 +821,14 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
+        c->edge_flag = env_long("IBLB_EDGE_FLAG", 1) != 0;
+        if (!c->sig) {
+            int rc = alloc_zero(c, (void**)&c->sig, 64);
+            if (rc) return rc;
+            HIP_TRY(c, hipHostMalloc((void**)&c->sig_err, 64, hipHostMallocCoherent));
+            *c->sig_err = 0;
+            c->sig_n = 0;
+        }
         c->bnd_w = INT_MAX;
         c->rccl_last = nullptr;  // the attach's all-gather is complete (synchronised above)
     }

@@ -435,6 +435,8 @@ void iblb_destroy(iblb_ctx* c) {
                     c->d_sch_us, c->d_sch_eps};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
+    if (c->sig) (void)hipFree(c->sig);
+    if (c->sig_err) (void)hipHostFree(c->sig_err);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->left && c->left->right == c) c->left->right = nullptr;
     if (c->right && c->right->left == c) c->right->left = nullptr;
@@ -792,7 +794,7 @@ int iblb_synchronize(iblb_ctx* c) {
     HIP_TRY(c, hipSetDevice(c->device));
     for (hipStream_t s : {c->stream, c->comm_stream, c->band_st, c->deep_st})
         if (s) HIP_TRY(c, hipStreamSynchronize(s));
-    return IBLB_OK;
+    return check_wait_err(c);
 }
 
 // ---- output gather (RCCL group) -----------------------------------------------------------------

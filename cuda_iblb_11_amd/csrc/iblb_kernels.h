@@ -104,6 +104,15 @@ struct Sweep2Args {
     double* Q;
     Coef c;
     KConst k;            // collide constants folded on the host (iblb_device.h)
+    // A slab interior's edge waves (ghost-column builds only): a wave whose output columns reach
+    // below wait_lo or above wait_hi first waits until *wait_seq - wait_val >= 0 (the comm stream's
+    // boundary sweeps of the previous cycle are done: they wrote the columns this wave pulls and read
+    // the ones it overwrites), bounded: after ~1 s it sets *wait_err and goes on (the host reports it).
+    // nullptr: no wait (the launch is ordered by its stream).
+    const unsigned* wait_seq = nullptr;
+    unsigned wait_val = 0;
+    int wait_lo = 0, wait_hi = 0;
+    unsigned* wait_err = nullptr;
     int nskip = 0;       // > 0: the patch output regions below are left to the band's last level,
     SkipBox skip[MAX_SKIP];  // sorted by x0, disjoint in columns (lone slab only)
 };
@@ -119,6 +128,9 @@ hipError_t launch_sweep2(Sweep2Args<T> a, bool ghost, hipStream_t s);
 template <typename T>
 hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool ghost, hipStream_t s, hipEvent_t stop = nullptr,
                          hipEvent_t start = nullptr);
+// *p = v after the stream's previous work (one lane, an agent-scope store: the release of the
+// previous kernel's stores is its end-of-kernel fence)
+hipError_t launch_seq_signal(unsigned* p, unsigned v, hipStream_t s);
 // Resident waves per CU of a deep-sweep configuration; *nch = its row chunks for ny rows.
 template <typename T>
 int sweepk_geometry(int depth, int vs, int variant, bool ghost, int ny, int* nch);

@@ -57,6 +57,16 @@ hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool slab, hipStream_t s, h
                 : launch_sweepk_slab<T, false>(a, depth, s, stop, start);
 }
 
+// the comm stream's "boundary sweeps done" signal (lbm_sweep_impl.h:edge_wait): a vector store of
+// one lane with agent scope; the boundary kernel's stores were released by its end-of-kernel fence
+__global__ __launch_bounds__(64) void seq_signal_kernel(unsigned* p, unsigned v) {
+    if (threadIdx.x == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+hipError_t launch_seq_signal(unsigned* p, unsigned v, hipStream_t s) {
+    seq_signal_kernel<<<1, 64, 0, s>>>(p, v);
+    return hipGetLastError();
+}
+
 template hipError_t launch_sweep2<double>(Sweep2Args<double>, bool, hipStream_t);
 template hipError_t launch_sweep2<float>(Sweep2Args<float>, bool, hipStream_t);
 template hipError_t launch_sweepk<double>(Sweep2Args<double>, int, bool, hipStream_t, hipEvent_t, hipEvent_t);

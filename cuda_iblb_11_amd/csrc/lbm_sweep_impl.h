@@ -827,6 +827,31 @@ __device__ __forceinline__ void split_item(const int nin, const int nsw_in, int 
     }
 }
 
+// A slab interior's edge wave waits for the comm stream's boundary sweeps of the previous cycle
+// (Sweep2Args::wait_seq) instead of the whole launch waiting behind a cross-queue barrier packet
+// (~9 us per cycle, profiles/r04/bsplit).  The protocol of MI355X_MICROARCH.md (inter-workgroup
+// visibility): the producer's stores are released by its kernel's end-of-kernel fence, then a
+// signal kernel stores the sequence number (agent scope); here one relaxed agent-scope poll per
+// ~0.2 us (s_sleep), then an agent-scope acquire (this CU's L1) drained by vmcnt(0) before the
+// wave's first load.  Each waiting wave acquires for itself, so no workgroup barrier is needed.
+// Bounded: a signal that never comes (the comm stream failed) must not leave the grid spinning.
+__device__ __forceinline__ void edge_wait(const unsigned* seq, unsigned val, unsigned* err) {
+    constexpr unsigned LIMIT = 1u << 23;  // x ~0.25 us per poll: ~2 s
+    unsigned n = 0;
+    for (;;) {
+        const unsigned s = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if ((int)(s - val) >= 0) break;
+        if (++n > LIMIT) {
+            if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // G ghost lanes at each wave edge (G * VS >= K - 1 rows)
 template <typename T, int VS, int MODE, int K, bool SLAB, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void sweepk_kernel(Sweep2Args<T> a) {
@@ -858,6 +883,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         xa = a.col_begin + (int)(sw * n / nsw);
         xb = a.col_begin + (int)((sw + 1) * n / nsw);
     }
+    if constexpr (SLAB)
+        if (a.wait_seq && (xa < a.wait_lo || xb > a.wait_hi)) edge_wait(a.wait_seq, a.wait_val, a.wait_err);
     const bool rev = sw & 1;
     double q;
     if ((MODE & MODE_SPLIT) && wall) {  // a wall chunk: one cell per lane, the wall walk

@@ -5,8 +5,18 @@ the last 100 cycles and the mean gap between consecutive interior sweeps (the cy
 import csv, glob, re, statistics, sys
 
 
-def kind(name):
-    if "sweepk_kernel" in name:  # sweepk_kernel<T, VS, MODE, K, SLAB[, WPE]>: SLAB = the boundary sweeps
+def grid_threads(r):
+    for k in ("Grid_Size", "Grid_Size_X", "Grid_SizeX"):
+        if k in r and r[k]:
+            return int(r[k])
+    return 0
+
+
+def kind(name, r=None):
+    if "sweepk_kernel" in name:  # sweepk_kernel<T, VS, MODE, K, SLAB[, WPE]>: SLAB = the boundary sweeps,
+        # or (round 5, the edge flag) a ghost-column interior: told apart by the grid (>= 64 workgroups)
+        if r is not None and grid_threads(r) >= 64 * 256:
+            return "sweep"
         return "sweep_slab" if re.search(r",\s*true\s*(,\s*\d+\s*)?>", name) else "sweep"
     if "pack" in name:
         return "pack"
@@ -18,7 +28,7 @@ def kind(name):
 def main(d):
     f = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
-    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind(r["Kernel_Name"])) for r in rows)
+    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind(r["Kernel_Name"], r)) for r in rows)
     ints = [e for e in ev if e[2] == "sweep"]
     if len(ints) < 50:  # lone slab: every sweep is a SLAB=false launch
         ints = [e for e in ev if e[2].startswith("sweep")]
@@ -50,7 +60,7 @@ def host_lag(d):
         return
     api = {r["Correlation_Id"]: r for r in csv.DictReader(open(hs[0]))}
     ints = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Correlation_Id"]) for r in kt
-                  if kind(r["Kernel_Name"]) == "sweep")[-100:]
+                  if kind(r["Kernel_Name"], r) == "sweep")[-100:]
     lags, starts = [], []
     for a, b in zip(ints, ints[1:]):
         h = api.get(b[2])

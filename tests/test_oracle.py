@@ -308,6 +308,31 @@ def test_fs_float_ulp_flips(oracle):
     assert d(c, a) <= 1e-12, d(c, a)
 
 
+def test_ib_flip_envelope(oracle):
+    """The envelope the GPU's many-point IB test is bounded by, pinned: the
+    oracle against itself over that test's whole horizon (38 iterations = 5K + 3 at K = 7), with
+    every population multiplied by 1 + mag * n (n in {-2..2}) before every iteration — the scale of
+    a reordered fp64 collide (2^-52) up to a few ulps per operation chain (2^-48).  Reproduces
+    tests/golden/ib_flip_envelope.json exactly (tests/golden/make_ib_flip_envelope.py); the flips are
+    discrete near-ties of the float F_s sum: at 2^-52 a run either flips none (fields <= 1e-11) or the
+    same component (40 ulps, fields 7.1e-9, first at iteration 12); at 2^-48 tens of ulps and fields
+    up to 2e-8.  The GPU test asserts <= 2x the envelope's maxima."""
+    import json
+    import ib_flips
+    fix = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ib_flip_envelope.json")))
+    env = ib_flips.envelope(oracle)
+    for mag, rows in env.items():
+        for r, g in zip(rows, fix["runs"][mag]):
+            assert r["fs_ulps"] == g["fs_ulps"] and r["first_flip"] == g["first_flip"], (mag, r, g)
+            assert abs(r["fields"] - g["fields"]) <= 1e-3 * g["fields"], (mag, r, g)
+    tiny = env[repr(2.0 ** -52)]
+    assert {r["fs_ulps"] for r in tiny} == {0, 40}
+    assert all((r["fields"] <= 1e-11) if r["fs_ulps"] == 0 else (6e-9 < r["fields"] < 8e-9) for r in tiny)
+    big = env[repr(2.0 ** -48)]
+    assert 20 <= max(r["fs_ulps"] for r in big) <= 100 and 1e-8 <= max(r["fields"] for r in big) <= 3e-8
+    assert fix["max_fs_ulps"] == max(r["fs_ulps"] for rows in env.values() for r in rows)
+
+
 def test_f32_model_tracks_oracle(oracle):
     """tests/f32_model.py (the float32 floor the GPU f32 parity is judged against) is the oracle's
     iteration: 11 iterations from a perturbed 64 x 48 channel agree to float32 rounding."""
