@@ -94,6 +94,7 @@ _SIGS = {
     "iblb_destroy": ([_vp], None),
     "iblb_last_error": ([_vp], C.c_char_p),
     "iblb_version": ([], C.c_char_p),
+    "iblb_abi_version": ([], C.c_int),
     "iblb_device_count": ([C.POINTER(C.c_int)], C.c_int),
     "iblb_set_state": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
     "iblb_set_lagrangian": ([_vp, C.c_int, _vp, _vp, _vp], C.c_int),
@@ -110,6 +111,7 @@ _SIGS = {
     "iblb_count_nonfinite": ([_vp, C.POINTER(C.c_longlong)], C.c_int),
     "iblb_set_profiling": ([_vp, C.c_int], C.c_int),
     "iblb_get_timing": ([_vp, C.POINTER(Timing), C.c_int], C.c_int),
+    "iblb_get_timing_ex": ([_vp, C.POINTER(Timing), C.c_ulong, C.c_int], C.c_int),
     "iblb_get_stream": ([_vp, C.POINTER(_vp)], C.c_int),
     "iblb_synchronize": ([_vp], C.c_int),
     "iblb_link_local": ([C.POINTER(_vp), C.c_int], C.c_int),

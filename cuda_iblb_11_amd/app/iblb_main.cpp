@@ -289,6 +289,9 @@ int main(int argc, char* argv[]) {
     //--------------------------ITERATION LOOP----------------------------- (main.cu:817-1024)
     // iblb_step runs whole iterations; the loop stops at every iteration the reference writes
     // output after (it % INTERVAL == 0), at it == INTERVAL and at checkpoints.
+    const char* ng = getenv("IBLB_NAN_GUARD");
+    const bool nan_guard = !(ng && std::string(ng) == "0");
+    bool nan_warned = false;
     unsigned int it = it0;
     while (it < ITERATIONS) {
         unsigned int next = (it / INTERVAL) * INTERVAL;  // next output iteration >= it
@@ -302,16 +305,19 @@ int main(int argc, char* argv[]) {
         it = next;
 
         //----------------------------DATA OUTPUT------------------------------ (main.cu:938-1005)
+        long long bad = 0;  // non-finite populations at this output iteration
         if (it % INTERVAL == 0) {
-            // not in the reference (it writes NaN fields on): a diverged run stops here, loudly,
-            // on every rank (the count is collective)
-            long long bad = 0;
+            // not in the reference (it writes NaN fields on): a diverged run is reported at the first
+            // output iteration that sees it, on every rank (the count is collective); that iteration's
+            // output is written as the reference writes it, then the run stops with status 3 —
+            // unless IBLB_NAN_GUARD=0, which keeps the reference's behaviour (warn once, go on)
             if ((rc = iblb_count_nonfinite(ctx, &bad))) return die(ctx, rc, "iblb_count_nonfinite");
-            if (bad > 0) {
+            if (bad > 0 && !nan_warned) {
                 cerr << "IBLB: the run diverged: " << bad << " non-finite populations at iteration " << it
-                     << " (output and further iterations skipped)" << endl;
-                iblb_destroy(ctx);
-                return 3;
+                     << (nan_guard ? " (this iteration's output written, further iterations skipped)"
+                                   : " (IBLB_NAN_GUARD=0: the run goes on, as the reference's)")
+                     << endl;
+                nan_warned = true;
             }
             if (BigData) {
                 if ((rc = iblb_gather_macro(ctx, 0, lead ? rho.data() : nullptr, lead ? u.data() : nullptr)))
@@ -345,6 +351,10 @@ int main(int argc, char* argv[]) {
                 fsB.open(flux.c_str(), ofstream::app);
                 fsB << it * t_scale << "\t" << Q * x_scale << endl;
                 fsB.close();
+            }
+            if (bad > 0 && nan_guard) {
+                iblb_destroy(ctx);
+                return 3;
             }
         }
 

@@ -74,6 +74,8 @@ struct iblb_ctx {
     int sweep_depth = 5;        // K iterations per deep launch (IBLB_SWEEP_DEPTH; 2 = two-step only)
     int deep_w = 96, deep_vs = 2, deep_variant = 1, deep_balance = 1;  // IBLB_DEEP_W / _VS / _VARIANT / _BALANCE
     int slab_vs = 1;            // cells per lane of a group slab's deep sweeps
+    int int_variant = -1;       // deep variant of a group slab's interior sweep (IBLB_INTERIOR_VARIANT; -1: deep_variant)
+    int edge_trim = 0;          // slab interiors: first / last sweep narrower by this (IBLB_EDGE_TRIM)
     int reserved_cus = 0, ncu = 0;  // CUs kept free of the compute stream (RCCL groups), device CUs
     std::vector<uint32_t> comp_mask;  // the compute stream's CU mask when reserved_cus > 0
     hipStream_t stream = nullptr;
@@ -146,7 +148,7 @@ struct iblb_ctx {
     uint8_t* bfl_alloc = nullptr;  // ... and their chunk flags (zero between cycles)
     double* bfd[2] = {nullptr, nullptr};
     uint8_t* bfl[2] = {nullptr, nullptr};
-    int band_par_env = 1;        // IBLB_BAND_PAR: a lone slab's last level beside the deep sweep
+    int band_par_env = 1;        // IBLB_BAND_PAR: the last level beside the deep sweep (lone and group slabs)
     bool band_par = false;       // the installed plan runs it (patch output rows skipped by the deep sweep)
     bool band_prev_par = false;  // the last band cycle ran it (its deep sweep ended on ev_deep)
     std::vector<iblb::SkipBox> band_skip;  // the plan's patch output regions (own columns, even rows)
@@ -189,8 +191,11 @@ struct iblb_ctx {
     // deep slab cycles: the interior's edge waves wait on a device word the comm stream's boundary
     // sweeps signal (IBLB_EDGE_FLAG, default on) instead of the compute queue waiting for ev_bnd
     bool edge_flag = true;
-    unsigned* sig = nullptr;      // device word: sequence number of the last boundary launch done
+    unsigned* sig = nullptr;      // device words: [0] sequence number of the last boundary launch done,
+                                  // [16] edge waves of the slab interiors done (ctx_step.hip:deep_slab_step)
     unsigned sig_n = 0;           // boundary launches signalled so far (the value of the last one)
+    unsigned done_n = 0;          // interior edge waves launched so far (the done word's value once they end)
+    bool int_unrec = false;       // the last interior carried no event: ev_int is recorded on demand
     unsigned* sig_err = nullptr;  // host-coherent word: an edge wave's bounded wait timed out
     // profiling
     bool prof = false;

@@ -65,8 +65,13 @@ int fill_ghosts_periodic(iblb_ctx* c, int which, int d, hipStream_t st) {
 
 // the comm stream is about to send the d edge columns of the current state: follow the compute
 // work of the last step unless the comm stream wrote them itself
+static int int_event(iblb_ctx* c);
 static int comm_ready(iblb_ctx* c, int d) {
-    if (d > c->bnd_w) HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_int, 0));
+    if (d > c->bnd_w) {
+        int rc = int_event(c);
+        if (rc) return rc;
+        HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_int, 0));
+    }
     return IBLB_OK;
 }
 
@@ -169,6 +174,7 @@ static int comm_follows(iblb_ctx* c) {
     HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
     HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_bnd, 0));
+    c->int_unrec = false;
     c->bnd_w = INT_MAX;
     return IBLB_OK;
 }
@@ -203,7 +209,7 @@ static int advance(iblb_ctx* c) {
 template <typename T>
 static int overlapped_step(iblb_ctx* c) {
     int rc = comm_ready(c, 1);
-    if (rc || (rc = exchange(c, c->comm_stream, 1))) return rc;
+    if (rc || (rc = exchange(c, c->comm_stream, 1)) || (rc = int_event(c))) return rc;
     HIP_TRY(c, hipStreamWaitEvent(c->comm_stream, c->ev_int, 0));
     if ((rc = launch_fused_step<T>(c, 0, 2, c->ncol - 1, false, c->comm_stream))) return rc;
     HIP_TRY(c, hipEventRecord(c->ev_bnd, c->comm_stream));
@@ -229,6 +235,7 @@ static int ib_overlapped_step(iblb_ctx* c, int next) {
     int rc = ib_ghost(c, c->g[c->cur], 0, 0, c->ncol, pts_s(c), pts_us(c), pts_eps(c), 1, c->stream);
     if (rc) return rc;
     HIP_TRY(c, hipEventRecord(c->ev_pre, c->stream));
+    if ((rc = int_event(c))) return rc;
     HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
     if ((rc = exchange(c, bs, 3))) return rc;
     if ((rc = ib_ghost(c, c->g[c->cur], 3, 0, c->ncol, pts_s(c), pts_us(c), pts_eps(c), 2, bs))) return rc;
@@ -313,6 +320,7 @@ static int sweep_step(iblb_ctx* c) {
     hipStream_t bs = ov ? c->comm_stream : c->stream;
     if (ov && (rc = comm_ready(c, 2))) return rc;
     if ((rc = exchange(c, bs, 2))) return rc;
+    if (ov && (rc = int_event(c))) return rc;
     if (ov) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_int, 0));
     if ((rc = sweep_launch<T>(c, sweep_args<T>(c, 0, c->ncol - 2, c->ncol, 2, 2), true, bs, false, 0))) return rc;
     if (ov) HIP_TRY(c, hipEventRecord(c->ev_bnd, bs));
@@ -365,25 +373,51 @@ static int sweepk_step(iblb_ctx* c, int d) {
 // K may differ from the previous cycle's (deep_depth): the exchange waits for the previous interior
 // when it sends columns that interior wrote (comm_ready: K > bnd_w), and every ghost column read is
 // within gc = 3 sweep_depth.
-// Edge flag (round 5, IBLB_EDGE_FLAG=1 default): in a chain of cycles the compute stream no longer
-// waits for boundary(t-K) (a barrier packet that cost ~9 us between consecutive interiors although
-// it was satisfied long before, profiles/r04/bsplit).  Only the interior's first and last sweeps
-// depend on boundary(t-K) — they pull columns [0, K) / [ncol-K, ncol) it wrote and overwrite
-// columns [K, 2K) / [ncol-2K, ncol-K) it read — so those waves wait on a device word the comm
-// stream sets after boundary(t-K) (a signal kernel: launch_seq_signal), with a bounded poll
-// (lbm_sweep_impl.h:edge_wait); every other wave starts at once.  The interior is then launched as
-// a ghost-column build (it reads no ghost column: the same cells, addressed without the periodic
-// wrap).  Deadlock freedom with shared hardware queues: DESIGN.md §8 (the wait graph).
+// Device handshake (round 5, IBLB_EDGE_FLAG=1 default).  Only the interior's first and last sweeps
+// (its edge waves) touch what the comm stream's boundary sweeps touch: they pull columns [0, K) /
+// [ncol-K, ncol) that boundary(t-K) wrote and overwrite [K, 2K) / [ncol-2K, ncol-K) that it read;
+// boundary(t+K) in turn reads what they write and overwrites what they read.  So in a chain of
+// cycles neither stream waits for the other in its queue:
+//   - interior(t)'s edge waves poll a word that a signal kernel after boundary(t-K) sets
+//     (launch_seq_signal) — the compute queue's barrier packet for ev_bnd cost ~9 us per cycle
+//     (profiles/r04/bsplit, r05/edge);
+//   - interior(t) carries no completion event (any signal on it, kernel's own or a marker, cost ~5 us
+//     before the next interior, profiles/r05/gap); its edge waves count themselves into a second word
+//     when their stores are released (lbm_sweep_impl.h:edge_done), and boundary(t+K)'s waves poll it
+//     for the count interior(t) brings it to.
+// Both polls are bounded (lbm_sweep_impl.h:edge_wait).  Every other interior wave starts and ends
+// freely.  The interior is launched as a ghost-column build (it reads no ghost column: the same cells,
+// addressed without the periodic wrap).  Edge waves: outputs below lo = 2 sweep_depth + 2 or above
+// ncol - lo (every depth K - 1, K a call mixes).  Consumers of ev_int after the chain record it first
+// (int_unrec: the compute stream's last work is then that interior).  Deadlock freedom with shared
+// hardware queues: DESIGN.md §8 (the wait graph).
+// (no reserved CUs: the spinning waves could hold the slots the other stream's kernels need — off)
+static bool dev_handshake(const iblb_ctx* c) {
+    return c->overlap && c->edge_flag && c->sig && c->reserved_cus > 0;
+}
+
+// ev_int names the compute stream's last interior; after a handshake chain it is recorded on demand
+static int int_event(iblb_ctx* c) {
+    if (c->int_unrec) {
+        HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
+        c->int_unrec = false;
+    }
+    return IBLB_OK;
+}
+
 template <typename T>
 static int deep_slab_step(iblb_ctx* c, int K) {
     const int W = std::max(1, c->deep_w);
     const bool ov = c->overlap;
     const bool chained = ov && c->deep_chain && c->deep_chain_t == c->t && c->deep_chain_cur == c->cur;
-    const bool flag = chained && c->edge_flag && c->sig;
+    const bool hs = dev_handshake(c);
+    const bool flag = chained && hs;  // device waits in both directions (else queue waits)
+    const int lo = 2 * c->sweep_depth + 2, hi = c->ncol - lo;
     int rc = flag ? IBLB_OK : join_comm(c);
     if (rc) return rc;
     hipStream_t bs = ov ? c->comm_stream : c->stream;
     const int ni = c->ncol - 2 * K;  // interior [K, ncol-K): needs nothing from the halo
+    const unsigned done_prev = c->done_n;  // the edge count interior(t-K) brought the done word to
     auto interior = [&](hipEvent_t stop) -> int {
         if (ni <= 0) {
             if (stop) HIP_TRY(c, hipEventRecord(stop, c->stream));
@@ -392,24 +426,38 @@ static int deep_slab_step(iblb_ctx* c, int K) {
         Sweep2Args<T> a = sweep_args<T>(c, K, c->deep_balance ? 0 : W, c->ncol - K, (ni + W - 1) / W, W);
         a.vs = c->slab_vs;
         a.cus = c->ncu - c->reserved_cus;  // the compute stream's CU mask
-        a.variant = c->deep_variant;
-        if (flag) {  // the value boundary(t-K) signalled; waves with outputs in [K, 2K) or [ncol-2K, ncol-K)
-            a.wait_seq = c->sig;
-            a.wait_val = c->sig_n;
-            a.wait_lo = 2 * K;
-            a.wait_hi = c->ncol - 2 * K;
-            a.wait_err = c->sig_err;
+        a.variant = c->int_variant >= 0 ? c->int_variant : c->deep_variant;
+        int nedge = 0;
+        if (hs) {
+            a.wait_lo = lo;
+            a.wait_hi = hi;
+            a.edge_trim = c->edge_trim;
+            a.done_cnt = c->sig + 16;  // (the done word: its own 64-byte line)
+            a.edge_waves = &nedge;
+            if (flag) {  // the value boundary(t-K)'s signal kernel stores
+                a.wait_seq = c->sig;
+                a.wait_val = c->sig_n;
+                a.wait_err = c->sig_err;
+            }
         }
         size_t ev = 0;
         int r = ev_begin(c, &ev, c->stream);
         if (r) return r;
-        HIP_TRY(c, launch_sweepk<T>(a, K, flag, c->stream, stop));
+        HIP_TRY(c, launch_sweepk<T>(a, K, hs, c->stream, stop));
+        c->done_n += (unsigned)nedge;
         return ev_end(c, ev, EV_SWEEPK, (long long)ni * c->ny, c->stream);
     };
     auto boundary = [&](hipEvent_t stop) -> int {
         Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
         b.vs = c->slab_vs;
         b.variant = c->deep_variant;
+        if (flag) {  // every wave waits for interior(t-K)'s edge waves
+            b.wait_seq = c->sig + 16;
+            b.wait_val = done_prev;
+            b.wait_lo = INT_MAX;
+            b.wait_hi = INT_MAX;
+            b.wait_err = c->sig_err;
+        }
         HIP_TRY(c, launch_sweepk<T>(b, K, true, bs, stop));
         return IBLB_OK;
     };
@@ -420,15 +468,24 @@ static int deep_slab_step(iblb_ctx* c, int K) {
     } else {
         // prev: the compute stream's work before interior(t) (interior(t-K) when chained)
         hipEvent_t prev = c->ev_int, next = c->ev_int2;
-        if (!chained) HIP_TRY(c, hipEventRecord(prev, c->stream));
-        if ((rc = interior(next))) return rc;
+        if (!chained) {
+            HIP_TRY(c, hipEventRecord(prev, c->stream));
+            c->int_unrec = false;
+        } else if (c->int_unrec && K > c->bnd_w) {  // the exchange below sends columns interior(t-K) wrote
+            if ((rc = int_event(c))) return rc;
+        }
+        if ((rc = interior(hs ? nullptr : next))) return rc;
         if ((rc = comm_ready(c, K))) return rc;  // (waits for c->ev_int = prev)
         if ((rc = exchange(c, bs, K))) return rc;
-        HIP_TRY(c, hipStreamWaitEvent(bs, prev, 0));
+        if (!flag) HIP_TRY(c, hipStreamWaitEvent(bs, prev, 0));
         if ((rc = boundary(c->ev_bnd))) return rc;
-        if (c->edge_flag && c->sig) HIP_TRY(c, launch_seq_signal(c->sig, ++c->sig_n, bs));
-        c->ev_int = next;
-        c->ev_int2 = prev;
+        if (hs) {
+            HIP_TRY(c, launch_seq_signal(c->sig, ++c->sig_n, bs));
+            c->int_unrec = true;  // ev_int (= prev) is recorded when someone needs it
+        } else {
+            c->ev_int = next;
+            c->ev_int2 = prev;
+        }
         c->bnd_w = K;
         c->deep_chain = true;
     }
@@ -822,12 +879,15 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
         c->edge_flag = env_long("IBLB_EDGE_FLAG", 1) != 0;
+        c->int_variant = (int)env_long("IBLB_INTERIOR_VARIANT", -1);
+        c->edge_trim = (int)std::max(0L, env_long("IBLB_EDGE_TRIM", 0));
         if (!c->sig) {
-            int rc = alloc_zero(c, (void**)&c->sig, 64);
+            int rc = alloc_zero(c, (void**)&c->sig, 128);  // signal word, done word (+64 B)
             if (rc) return rc;
             HIP_TRY(c, hipHostMalloc((void**)&c->sig_err, 64, hipHostMallocCoherent));
             *c->sig_err = 0;
             c->sig_n = 0;
+            c->done_n = 0;
         }
         c->bnd_w = INT_MAX;
         c->rccl_last = nullptr;  // the attach's all-gather is complete (synchronised above)

@@ -267,7 +267,8 @@ static int reset_cilia_state(iblb_ctx* c) {
     return IBLB_OK;
 }
 
-const char* iblb_version(void) { return "iblb-mi355x 0.3 (gfx950)"; }
+const char* iblb_version(void) { return "iblb-mi355x 0.5 (gfx950, abi 5)"; }
+int iblb_abi_version(void) { return IBLB_ABI_VERSION; }
 
 int iblb_device_count(int* n) {
     if (!n) return IBLB_ERR_ARG;
@@ -746,8 +747,12 @@ int iblb_set_profiling(iblb_ctx* c, int enabled) {
     return IBLB_OK;
 }
 
-int iblb_get_timing(iblb_ctx* c, iblb_timing* t, int reset) {
-    if (!c || !t) return IBLB_ERR_ARG;
+int iblb_get_timing(iblb_ctx* c, iblb_timing* t, int reset) { return iblb_get_timing_ex(c, t, sizeof(*t), reset); }
+
+int iblb_get_timing_ex(iblb_ctx* c, iblb_timing* out, unsigned long bytes, int reset) {
+    if (!c || !out || bytes == 0) return IBLB_ERR_ARG;
+    iblb_timing full{};
+    iblb_timing* t = &full;
     HIP_TRY(c, hipSetDevice(c->device));
     for (hipStream_t s : {c->stream, c->comm_stream, c->band_st, c->deep_st})
         if (s) HIP_TRY(c, hipStreamSynchronize(s));
@@ -780,6 +785,7 @@ int iblb_get_timing(iblb_ctx* c, iblb_timing* t, int reset) {
         c->fused_launches = c->fused_cells = c->sweep_launches = c->sweep_cells = 0;
         c->sweepk_launches = c->sweepk_cells = 0;
     }
+    std::memcpy(out, &full, std::min((size_t)bytes, sizeof(full)));
     return IBLB_OK;
 }
 

@@ -72,7 +72,7 @@ struct FusedArgs {
 };
 
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.
-// IB band cycle with its last level beside the deep sweep (lone slab): a patch output region the
+// IB band cycle with its last level beside the deep sweep (and a group slab's boundary sweeps): a patch output region the
 // last level stores and the deep sweep must not: local columns [x0, x1] (inclusive) x rows [y0, y1)
 // (even bounds, so that a lane's two cells are both in or both out)
 struct SkipBox {
@@ -104,17 +104,21 @@ struct Sweep2Args {
     double* Q;
     Coef c;
     KConst k;            // collide constants folded on the host (iblb_device.h)
-    // A slab interior's edge waves (ghost-column builds only): a wave whose output columns reach
-    // below wait_lo or above wait_hi first waits until *wait_seq - wait_val >= 0 (the comm stream's
-    // boundary sweeps of the previous cycle are done: they wrote the columns this wave pulls and read
-    // the ones it overwrites), bounded: after ~1 s it sets *wait_err and goes on (the host reports it).
-    // nullptr: no wait (the launch is ordered by its stream).
+    // Device-side ordering of a slab's interior and boundary sweeps (ghost-column builds only,
+    // ctx_step.hip:deep_slab_step).  An edge wave is one whose output columns reach below wait_lo or
+    // above wait_hi (wait_lo = INT_MAX: every wave).  wait_seq: edge waves first wait until
+    // *wait_seq - wait_val >= 0 (bounded: after ~2 s they set *wait_err and go on; the host reports
+    // it).  done_cnt: edge waves add 1 when their stores are released (agent scope), and the host
+    // learns their number from *edge_waves (set by the launcher).  nullptr: no wait / no signal.
     const unsigned* wait_seq = nullptr;
     unsigned wait_val = 0;
     int wait_lo = 0, wait_hi = 0;
     unsigned* wait_err = nullptr;
+    unsigned* done_cnt = nullptr;
+    int* edge_waves = nullptr;  // host pointer, written by launch_sweepk (not read on the device)
+    int edge_trim = 0;          // balanced sweeps: the first and last sweep this many columns narrower
     int nskip = 0;       // > 0: the patch output regions below are left to the band's last level,
-    SkipBox skip[MAX_SKIP];  // sorted by x0, disjoint in columns (lone slab only)
+    SkipBox skip[MAX_SKIP];  // sorted by x0, disjoint in columns (a lone slab's deep sweep, a group slab's interior and boundary sweeps)
 };
 
 // ghost: false = lone slab (columns outside [0, ncol) are the periodic images; also the interior

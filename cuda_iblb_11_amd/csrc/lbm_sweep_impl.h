@@ -852,6 +852,26 @@ __device__ __forceinline__ void edge_wait(const unsigned* seq, unsigned val, uns
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// The edge wave's stores released, then counted (MI355X_MICROARCH.md, Valid forms: every storing
+// wave's vmcnt(0), the agent-scope release, the asm wait the compiler may otherwise drop after it,
+// then the agent-scope atomic add; each edge wave signals for itself).
+__device__ __forceinline__ void edge_done(unsigned* cnt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Balanced sweep s of nsw over [cb, ce): floor/ceil((ce - cb) / nsw) columns; trim > 0 makes the first
+// and last sweeps `trim` columns narrower (a slab interior's edge waves, which also wait and signal)
+__host__ __device__ inline void balanced_range(int cb, int ce, int trim, int s, int nsw, int& xa, int& xb) {
+    const long n = (long)(ce - cb) + 2L * trim;
+    xa = cb - trim + (int)(s * n / nsw);
+    xb = cb - trim + (int)((s + 1) * n / nsw);
+    xa = xa < cb ? cb : xa;
+    xb = xb > ce ? ce : xb;
+}
+
 // G ghost lanes at each wave edge (G * VS >= K - 1 rows)
 template <typename T, int VS, int MODE, int K, bool SLAB, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void sweepk_kernel(Sweep2Args<T> a) {
@@ -879,12 +899,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         xa = a.col_begin + sw * a.col_step;
         xb = min(xa + a.W, a.col_end);
     } else {  // balanced: nsw sweeps of floor/ceil((col_end - col_begin) / nsw) columns
-        const long n = a.col_end - a.col_begin;
-        xa = a.col_begin + (int)(sw * n / nsw);
-        xb = a.col_begin + (int)((sw + 1) * n / nsw);
+        balanced_range(a.col_begin, a.col_end, a.edge_trim, sw, nsw, xa, xb);
     }
+    const bool edge = SLAB && (xa < a.wait_lo || xb > a.wait_hi);
     if constexpr (SLAB)
-        if (a.wait_seq && (xa < a.wait_lo || xb > a.wait_hi)) edge_wait(a.wait_seq, a.wait_val, a.wait_err);
+        if (a.wait_seq && edge) edge_wait(a.wait_seq, a.wait_val, a.wait_err);
     const bool rev = sw & 1;
     double q;
     if ((MODE & MODE_SPLIT) && wall) {  // a wall chunk: one cell per lane, the wall walk
@@ -927,6 +946,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const double qs = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, qs);
     }
+    if constexpr (SLAB)
+        if (a.done_cnt && edge) edge_done(a.done_cnt);
 }
 
 // Waves of one instantiation resident per CU (256-thread workgroups), and on `cus` CUs (0: all).
@@ -990,6 +1011,24 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
         waves = (long)b.nsweep * b.wall_ch0 + 2L * b.nsweep_w;
     } else {
         waves = (long)b.nsweep * b.nch;
+    }
+    if (b.edge_waves) {  // the waves that will add to done_cnt (sweepk_kernel's `edge`)
+        auto edges = [&](int nsw) {
+            int e = 0;
+            for (int sw = 0; sw < nsw; ++sw) {
+                int xa, xb;
+                if (b.col_step > 0) {
+                    xa = b.col_begin + sw * b.col_step;
+                    xb = std::min(xa + b.W, b.col_end);
+                } else {
+                    balanced_range(b.col_begin, b.col_end, b.edge_trim, sw, nsw, xa, xb);
+                }
+                e += (xa < b.wait_lo || xb > b.wait_hi) ? 1 : 0;
+            }
+            return e;
+        };
+        *b.edge_waves = (MODE & MODE_SPLIT) ? edges(b.nsweep) * b.wall_ch0 + 2 * edges(b.nsweep_w)
+                                            : edges(b.nsweep) * b.nch;
     }
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     if (stop || start)  // the events ride on the kernel's own signals: no marker packets around it

@@ -259,7 +259,7 @@ class Lattice:
 
     def timing(self, reset: bool = False) -> dict:
         t = L.Timing()
-        self._check(self._lib.iblb_get_timing(self._h, C.byref(t), 1 if reset else 0))
+        self._check(self._lib.iblb_get_timing_ex(self._h, C.byref(t), C.sizeof(t), 1 if reset else 0))
         return {k: getattr(t, k) for k, _ in L.Timing._fields_}
 
     @property

@@ -20,8 +20,9 @@
  *      x-slab of the lattice on one GPU, stores the populations SoA (y fastest) and
  *      advances the exact reference time step
  *        equilibrium -> collision -> streaming -> macro -> interpolate -> spread
- *      (main.cu:852-909) with ONE bandwidth-bound kernel per step plus tiny IB
- *      kernels.  Host arrays crossing this boundary use the reference layouts
+ *      (main.cu:852-909): without IB one bandwidth-bound kernel advances up to seven
+ *      iterations (temporal blocking, the deep sweep), with IB a band cycle of K iterations
+ *      (the deep sweep beside a chain of small launches around the points).  Host arrays crossing this boundary use the reference layouts
  *      restricted to the slab: cell j = y * x_count + (x - x_begin).
  *
  * Conventions: every function returns IBLB_OK (0) or a negative IBLB_ERR_* code;
@@ -51,6 +52,11 @@ extern "C" {
 #define IBLB_PREC_F32 1          /* populations stored as float deviations f - w_i */
 
 #define IBLB_UNIQUE_ID_BYTES 128 /* size of the RCCL unique id blob               */
+
+/* ABI version of this header: bumped whenever a struct crossing the ABI changes layout (iblb_config,
+ * iblb_timing, iblb_cilia).  5: iblb_timing's band_cycles ... deep_iterations (round 4), the
+ * size-checked iblb_get_timing_ex (round 5).  Compare with iblb_abi_version() at run time. */
+#define IBLB_ABI_VERSION 5
 
 /* ---------------------------------------------------------------------------------
  * (1) Reference-shaped kernels.  All pointers are DEVICE pointers.  `stream` is a
@@ -166,6 +172,7 @@ int  iblb_create(const iblb_config* cfg, iblb_ctx** out);
 void iblb_destroy(iblb_ctx* ctx);
 const char* iblb_last_error(const iblb_ctx* ctx);   /* NULL ctx: last create() error */
 const char* iblb_version(void);
+int  iblb_abi_version(void);                       /* IBLB_ABI_VERSION the library was built with */
 int  iblb_device_count(int* n);
 
 /* Initial state (main.cu:636-754).  rho [N], u [2N] SoA, force [2N] SoA (force^0, may be
@@ -233,6 +240,10 @@ int iblb_count_nonfinite(iblb_ctx* ctx, long long* count);
  * stream it runs on; iblb_get_timing() returns the sums (and resets them if reset). */
 int iblb_set_profiling(iblb_ctx* ctx, int enabled);
 int iblb_get_timing(iblb_ctx* ctx, iblb_timing* t, int reset);
+/* The same, writing at most `bytes` bytes of the struct (pass sizeof(iblb_timing) of the header the
+ * caller was built with: an older, shorter iblb_timing gets its own fields only).  iblb_get_timing
+ * writes sizeof(iblb_timing) of THIS header. */
+int iblb_get_timing_ex(iblb_ctx* ctx, iblb_timing* t, unsigned long bytes, int reset);
 /* The stream the context launches on (hipStream_t), for callers that add work. */
 int iblb_get_stream(iblb_ctx* ctx, void** stream);
 /* Block until all work of the context is done. */

@@ -105,6 +105,7 @@ def main():
 
     uid = rccl_unique_id(lib)
     out = [None] * n
+    par = [0] * n
     gathered = [None] * n
     restarted = [None] * n
     errors = []
@@ -163,8 +164,11 @@ def main():
             if with_ib:
                 lat.set_lagrangian(*pts(it))
             lat.step(1)
-        if band and lat.timing()["sweepk_launches"] == 0:
-            raise RuntimeError(f"rank {r}: the band cycle did not run")
+        if band:
+            tm = lat.timing()
+            if tm["sweepk_launches"] == 0:
+                raise RuntimeError(f"rank {r}: the band cycle did not run")
+            par[r] = tm["band_par_cycles"]
         rs, us = lat.macro()
         out[r] = (xb, xc, rs, us, lat.flux, lat.lagrangian_force() if with_ib else None)  # collective
         gathered[r] = lat.gather_macro(0)  # collective output gather to rank 0
@@ -236,7 +240,7 @@ def main():
         ok = ok and max(d_oracle.values()) <= (1e-9 if prec == "f64" else 1e-4)
     print(json.dumps({"ok": bool(ok), "exact": exact, "d_rho": d_rho, "d_u": d_u, "d_flux": d_q, "n": n,
                       "gather_ok": g_ok, "restart_ok": bool(rs_ok), "d_restart": d_re, "d_F_s": d_fs,
-                      "with_ib": with_ib, "precision": prec, "d_oracle": d_oracle}), flush=True)
+                      "with_ib": with_ib, "precision": prec, "d_oracle": d_oracle, "band_par_cycles": par}), flush=True)
     sys.exit(0 if ok else 1)
 
 

@@ -112,3 +112,15 @@ def test_struct_layouts_match_the_header(tmp_path):
         assert got[(cname, "size")] == C.sizeof(py), cname
         for fname, _ in py._fields_:
             assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
+
+
+def test_abi_version_matches_header():
+    """IBLB_ABI_VERSION of include/iblb.h is what the library was built with (a struct crossing the ABI
+    changed layout: the version moves), and iblb_get_timing_ex exists for callers of older headers."""
+    import re
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "iblb.h")).read()
+    v = int(re.search(r"#define IBLB_ABI_VERSION (\d+)", hdr).group(1))
+    lib = L.load()
+    assert lib.iblb_abi_version() == v
+    assert f"abi {v}" in lib.iblb_version().decode()
+    assert lib.iblb_get_timing_ex(None, None, 0, 0) == L.IBLB_ERR_ARG

@@ -167,7 +167,29 @@ def test_app_stops_a_diverged_run(gpu, tmp_path):
     the reference writes NaN fields on; the driver checks the populations at every output
     iteration (iblb_count_nonfinite, collective) and stops with status 3 instead."""
     args = ARGS[:6] + ["0.001", "10"] + ARGS[8:]  # 100 iterations, output every 10
-    assert M.params(args)["ITERATIONS"] == 100
+    p = M.params(args)
+    assert p["ITERATIONS"] == 100
     r = run_app(args, tmp_path)
     assert r.returncode == 3, r.stdout + r.stderr
     assert "the run diverged" in r.stderr, r.stderr
+    # the diverged iteration's output is written as the reference writes it (NaN fields), then the
+    # run stops: the flux file ends at that iteration (no final line)
+    it = int(r.stderr.split("populations at iteration ")[1].split()[0])
+    assert 10 <= it < 100 and it % 10 == 0, r.stderr
+    fluid = read(tmp_path, M.paths(p)["raw"] + f"{it}-fluid.dat")
+    assert "nan" in fluid.lower()
+    assert not os.path.exists(str(tmp_path) + "/" + M.paths(p)["raw"] + f"{it + 10}-fluid.dat")
+    assert len(read(tmp_path, M.paths(p)["flux"]).strip().split("\n")) == it // 10 + 1
+
+
+@pytest.mark.gpu
+def test_app_nan_guard_off_keeps_reference_behaviour(gpu, tmp_path):
+    """IBLB_NAN_GUARD=0: the diverged run goes on to the end as the reference's does (NaN fields
+    written at every output iteration, the final flux line), with one warning."""
+    args = ARGS[:6] + ["0.001", "10"] + ARGS[8:]
+    p = M.params(args)
+    r = run_app(args, tmp_path, IBLB_NAN_GUARD=0)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stderr.count("the run diverged") == 1, r.stderr
+    assert os.path.exists(str(tmp_path) + "/" + M.paths(p)["raw"] + "90-fluid.dat")
+    assert len(read(tmp_path, M.paths(p)["flux"]).strip().split("\n")) == 11

@@ -349,6 +349,30 @@ def test_rccl_slab_band_cycle_threads_chain(gpu, n, precision, merge, monkeypatc
     test_rccl_slab_path_threads(gpu, n, "3", precision, 1, 1, 5, nx=48 * n)
 
 
+@pytest.mark.parametrize("n,par", [(2, "2"), (2, "0"), (4, "2"), (4, "0")])
+def test_rccl_slab_band_par(gpu, n, par, monkeypatch):
+    """IBLB_BAND_PAR on group slabs: the last level beside the deep and boundary sweeps,
+    which skip the patch output rows (MODE_SKIP), forced on (2) and off (0) for f64 slabs with a moving
+    filament across every slab edge (mode 3).  Both must equal the single slab stepped one iteration at
+    a time within 1e-12 (so within 2e-12 of each other) and the oracle within 1e-9; PAR must run
+    on every rank when forced and on none when off."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, IBLB_OVERLAP="1", IBLB_SWEEP_DEPTH="5", GPU_MAX_HW_QUEUES="16", IBLB_BAND_PAR=par)
+    cmd = [sys.executable, os.path.join(here, "mock_rccl", "run_group.py"), str(n), str(48 * n), "130", "25", "3",
+           "f64", "1"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines, p.stdout + p.stderr
+    res = json.loads(lines[-1])
+    assert p.returncode == 0 and res["ok"], (res, p.stderr[-2000:])
+    assert res["d_rho"] <= 1e-12 and res["d_u"] <= 1e-12, res
+    assert (all(c > 0 for c in res["band_par_cycles"]) if par == "2" else not any(res["band_par_cycles"])), res
+
+
 @pytest.mark.parametrize("n,workload,merge", [(2, "K4", None), (4, "K4", None), (8, "K4", None),
                                               (2, "K5", None), (4, "K5", None), (8, "K5", None),
                                               (8, "K5", "0"), (2, "K5", "2")])
