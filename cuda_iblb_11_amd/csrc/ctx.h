@@ -190,7 +190,7 @@ struct iblb_ctx {
     bool overlap = true;          // IBLB_OVERLAP
     // deep slab cycles: the interior's edge waves wait on a device word the comm stream's boundary
     // sweeps signal (IBLB_EDGE_FLAG, default on) instead of the compute queue waiting for ev_bnd
-    bool edge_flag = true;
+    int edge_flag = 1;  // 1: two-way device handshake, 2: one way (interior waits only), 0: queue waits
     unsigned* sig = nullptr;      // device words: [0] sequence number of the last boundary launch done,
                                   // [16] edge waves of the slab interiors done (ctx_step.hip:deep_slab_step)
     unsigned sig_n = 0;           // boundary launches signalled so far (the value of the last one)
@@ -198,7 +198,7 @@ struct iblb_ctx {
     bool int_unrec = false;       // the last interior carried no event: ev_int is recorded on demand
     unsigned* sig_err = nullptr;  // host-coherent word: an edge wave's bounded wait timed out
     // profiling
-    bool prof = false;
+    int prof = 0;  // 1: events around every launch; 2: the deep launches' own signals only (iblb_set_profiling)
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     double fused_ms = 0., ib_ms = 0., halo_ms = 0., sweep_ms = 0., sweepk_ms = 0.;

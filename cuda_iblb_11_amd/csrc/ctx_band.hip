@@ -421,12 +421,14 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
         std::copy(c->band_skip.begin(), c->band_skip.end(), d.skip);
     }
     size_t ev = 0;
-    int rc = ev_begin(c, &ev, ds);
+    hipEvent_t e0, e1;  // timing on the launch's own signals (profiling only)
+    int rc = ev_kernel(c, &ev, &e0, &e1);
     if (rc) return rc;
-    HIP_TRY(c, launch_sweepk<T>(d, K, false, ds, c->band_par ? c->ev_deep : nullptr));
+    HIP_TRY(c, launch_sweepk<T>(d, K, false, ds, e1 ? e1 : (c->band_par ? c->ev_deep : nullptr), e0));
+    if (e1 && c->band_par) HIP_TRY(c, hipEventRecord(c->ev_deep, ds));
     c->deep_launches++;
     c->deep_iterations += K;
-    return ev_end(c, ev, EV_SWEEPK, (long long)n * c->ny, ds);
+    return ev_kernel_end(c, ev, EV_SWEEPK, (long long)n * c->ny);
 }
 
 // Columns the force of level j may be spread into (the band trapezoid's [clo, chi)).  Chained

@@ -395,6 +395,9 @@ static int sweepk_step(iblb_ctx* c, int d) {
 static bool dev_handshake(const iblb_ctx* c) {
     return c->overlap && c->edge_flag && c->sig && c->reserved_cus > 0;
 }
+// IBLB_EDGE_FLAG=2: one way only (the interior's edge waves wait on the device word; the comm stream
+// waits for the interior's completion event in its queue) — round 5's first step, kept for A/B
+static bool one_way(const iblb_ctx* c) { return c->edge_flag == 2; }
 
 // ev_int names the compute stream's last interior; after a handshake chain it is recorded on demand
 static int int_event(iblb_ctx* c) {
@@ -432,8 +435,10 @@ static int deep_slab_step(iblb_ctx* c, int K) {
             a.wait_lo = lo;
             a.wait_hi = hi;
             a.edge_trim = c->edge_trim;
-            a.done_cnt = c->sig + 16;  // (the done word: its own 64-byte line)
-            a.edge_waves = &nedge;
+            if (!one_way(c)) {
+                a.done_cnt = c->sig + 16;  // (the done word: its own 64-byte line)
+                a.edge_waves = &nedge;
+            }
             if (flag) {  // the value boundary(t-K)'s signal kernel stores
                 a.wait_seq = c->sig;
                 a.wait_val = c->sig_n;
@@ -441,17 +446,19 @@ static int deep_slab_step(iblb_ctx* c, int K) {
             }
         }
         size_t ev = 0;
-        int r = ev_begin(c, &ev, c->stream);
+        hipEvent_t e0, e1;  // timing on the launch's own signals (profiling only)
+        int r = ev_kernel(c, &ev, &e0, &e1);
         if (r) return r;
-        HIP_TRY(c, launch_sweepk<T>(a, K, hs, c->stream, stop));
+        HIP_TRY(c, launch_sweepk<T>(a, K, hs, c->stream, e1 ? e1 : stop, e0));
+        if (e1 && stop) HIP_TRY(c, hipEventRecord(stop, c->stream));
         c->done_n += (unsigned)nedge;
-        return ev_end(c, ev, EV_SWEEPK, (long long)ni * c->ny, c->stream);
+        return ev_kernel_end(c, ev, EV_SWEEPK, (long long)ni * c->ny);
     };
     auto boundary = [&](hipEvent_t stop) -> int {
         Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
         b.vs = c->slab_vs;
         b.variant = c->deep_variant;
-        if (flag) {  // every wave waits for interior(t-K)'s edge waves
+        if (flag && !one_way(c)) {  // every wave waits for interior(t-K)'s edge waves
             b.wait_seq = c->sig + 16;
             b.wait_val = done_prev;
             b.wait_lo = INT_MAX;
@@ -474,13 +481,14 @@ static int deep_slab_step(iblb_ctx* c, int K) {
         } else if (c->int_unrec && K > c->bnd_w) {  // the exchange below sends columns interior(t-K) wrote
             if ((rc = int_event(c))) return rc;
         }
-        if ((rc = interior(hs ? nullptr : next))) return rc;
+        const bool two = hs && !one_way(c);
+        if ((rc = interior(two ? nullptr : next))) return rc;
         if ((rc = comm_ready(c, K))) return rc;  // (waits for c->ev_int = prev)
         if ((rc = exchange(c, bs, K))) return rc;
-        if (!flag) HIP_TRY(c, hipStreamWaitEvent(bs, prev, 0));
+        if (!(flag && two)) HIP_TRY(c, hipStreamWaitEvent(bs, prev, 0));
         if ((rc = boundary(c->ev_bnd))) return rc;
-        if (hs) {
-            HIP_TRY(c, launch_seq_signal(c->sig, ++c->sig_n, bs));
+        if (hs) HIP_TRY(c, launch_seq_signal(c->sig, ++c->sig_n, bs));
+        if (two) {
             c->int_unrec = true;  // ev_int (= prev) is recorded when someone needs it
         } else {
             c->ev_int = next;
@@ -878,7 +886,7 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
-        c->edge_flag = env_long("IBLB_EDGE_FLAG", 1) != 0;
+        c->edge_flag = (int)env_long("IBLB_EDGE_FLAG", 1);
         c->int_variant = (int)env_long("IBLB_INTERIOR_VARIANT", -1);
         c->edge_trim = (int)std::max(0L, env_long("IBLB_EDGE_TRIM", 0));
         if (!c->sig) {

@@ -62,7 +62,7 @@ static int ev_reserve(iblb_ctx* c, size_t* idx) {
 }
 
 int ev_begin(iblb_ctx* c, size_t* idx, hipStream_t st) {
-    if (!c->prof) return IBLB_OK;
+    if (c->prof != 1) return IBLB_OK;  // (mode 2: only the deep launches' own signals)
     int rc = ev_reserve(c, idx);
     if (rc) return rc;
     HIP_TRY(c, hipEventRecord(c->ev_pool[*idx], st ? st : c->stream));
@@ -81,7 +81,7 @@ static int ev_note(iblb_ctx* c, size_t idx, int kind, long long cells) {
 }
 
 int ev_end(iblb_ctx* c, size_t idx, int kind, long long cells, hipStream_t st) {
-    if (!c->prof) return IBLB_OK;
+    if (c->prof != 1) return IBLB_OK;
     HIP_TRY(c, hipEventRecord(c->ev_pool[idx + 1], st ? st : c->stream));
     return ev_note(c, idx, kind, cells);
 }
@@ -743,7 +743,7 @@ int iblb_get_step(iblb_ctx* c, long long* steps) {
 
 int iblb_set_profiling(iblb_ctx* c, int enabled) {
     if (!c) return IBLB_ERR_ARG;
-    c->prof = enabled != 0;
+    c->prof = enabled == 2 ? 2 : enabled != 0 ? 1 : 0;
     return IBLB_OK;
 }
 

@@ -39,7 +39,8 @@ namespace iblb {
 
 // sweep only (MODE bits 1, 2 as in lbm_vec.h): no software prefetch of the next column (two-step
 // sweeps); the deep sweep's wall split (sweepk_kernel)
-enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16, MODE_PACK = 64, MODE_SKIP = 128, MODE_PRESHIFT = 256, MODE_LDSWIN = 512 };
+enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16, MODE_PACK = 64, MODE_SKIP = 128, MODE_PRESHIFT = 256, MODE_LDSWIN = 512,
+       MODE_WT_STORE = 1024 };
 
 namespace {
 
@@ -445,7 +446,9 @@ __device__ __forceinline__ void st_rows_buf(__amdgpu_buffer_rsrc_t r, unsigned v
     vec x;
 #pragma unroll
     for (int e = 0; e < VS; ++e) x[e] = v[e];
-    constexpr int aux = (MODE & MODE_NT_STORE) ? 2 : 0;
+    // MODE_WT_STORE (a slab interior's edge waves): sc1, write-through — the handed-off columns leave
+    // the XCD's L2 with the store, so the wave's signal needs no L2-wide release (Guideline 16 R1)
+    constexpr int aux = (MODE & MODE_WT_STORE) ? 16 : (MODE & MODE_NT_STORE) ? 2 : 0;
     constexpr int B = VS * (int)sizeof(T);
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
     typedef unsigned u2 __attribute__((ext_vector_type(2)));
@@ -660,9 +663,16 @@ __device__ __forceinline__ bool skip_rows(const Sweep2Args<T>& a, int c, int r0,
 // populations of the middle column: 256 VGPRs + 4 AGPRs instead of 256 + 142 at K = 7, no AGPR moves
 // in the walk (profiles/r04/ldswin).
 template <typename T, int VS, int MODE, bool WL>
-constexpr bool lds_window() { return (MODE & MODE_LDSWIN) && sizeof(T) == 8 && VS == 2 && !WL; }
-template <int K, int VS>
-constexpr int lds_window_wave() { return 2 * (K - 1) * 3 * 64 * VS; }  // elements per wave
+constexpr bool lds_window() { return (MODE & MODE_LDSWIN) && VS == 2 && !WL; }
+// the moving populations kept in LDS: f64 all three; f32 (three waves per SIMD, round 5) the two
+// diagonal ones, so that twelve waves' windows fit a CU's LDS (147 of 160 KB) — the third stays in
+// registers (a two-column rotation, like the register window)
+template <typename T>
+constexpr bool lds_pop(int k) { return sizeof(T) == 8 || cy(k) != 0; }
+template <typename T>
+constexpr int lds_npop() { return sizeof(T) == 8 ? 3 : 2; }
+template <typename T, int K, int VS>
+constexpr int lds_window_wave() { return 2 * (K - 1) * lds_npop<T>() * 64 * VS; }  // elements per wave
 
 template <typename T, int VS, int MODE, int K, bool SLAB, bool REV, bool LW>
 __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int nl1, int x0, int xa, int xb, int row0,
@@ -698,11 +708,11 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
         typedef typename VT<T, VS>::type vec;
         vec* ls = nullptr;
         if constexpr (LW) {  // slot of parity i: the column made two iterations ago, then this one's
-            ls = (vec*)(lw + ((i & 1) * (K - 1) + (l - 2)) * 3 * 64 * VS);
+            ls = (vec*)(lw + ((i & 1) * (K - 1) + (l - 2)) * lds_npop<T>() * 64 * VS);
             int p = 0;
 #pragma unroll
             for (int k = 0; k < 9; ++k)
-                if (cx(k) == DX) {
+                if (cx(k) == DX && lds_pop<T>(k)) {
                     const vec v = ls[p * 64];
 #pragma unroll
                     for (int e = 0; e < VS; ++e) WA[l - 2][k][e] = v[e];
@@ -724,11 +734,19 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
 #pragma unroll
             for (int k = 0; k < 9; ++k)
                 if (cx(k) == DX) {
-                    vec v;
+                    if (lds_pop<T>(k)) {
+                        vec v;
 #pragma unroll
-                    for (int e = 0; e < VS; ++e) v[e] = N[k][e];
-                    ls[p * 64] = v;
-                    ++p;
+                        for (int e = 0; e < VS; ++e) v[e] = N[k][e];
+                        ls[p * 64] = v;
+                        ++p;
+                    } else {  // (f32) the register rotation of this population
+#pragma unroll
+                        for (int e = 0; e < VS; ++e) {
+                            WA[l - 2][k][e] = WB[l - 2][k][e];
+                            WB[l - 2][k][e] = N[k][e];
+                        }
+                    }
                 }
 #pragma unroll
             for (int k = 0; k < 9; ++k)
@@ -855,10 +873,15 @@ __device__ __forceinline__ void edge_wait(const unsigned* seq, unsigned val, uns
 // The edge wave's stores released, then counted (MI355X_MICROARCH.md, Valid forms: every storing
 // wave's vmcnt(0), the agent-scope release, the asm wait the compiler may otherwise drop after it,
 // then the agent-scope atomic add; each edge wave signals for itself).
-__device__ __forceinline__ void edge_done(unsigned* cnt) {
+// wt: every store of the wave was write-through (sc1): drained by vmcnt(0), no release needed (R1).
+// (The L2-wide release of plain stores, one per edge wave, cost the 512-column interior 7 us per launch,
+// profiles/r05/hs.)
+__device__ __forceinline__ void edge_done(unsigned* cnt, bool wt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!wt) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -881,8 +904,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     T* lw = nullptr;
     if constexpr (lds_window<T, VS, MODE, false>()) {
-        __shared__ __attribute__((aligned(16))) T lwin[4 * lds_window_wave<K, VS>()];
-        lw = lwin + wv * lds_window_wave<K, VS>() + lane * VS;
+        __shared__ __attribute__((aligned(16))) T lwin[4 * lds_window_wave<T, K, VS>()];
+        lw = lwin + wv * lds_window_wave<T, K, VS>() + lane * VS;
     }
     int sw, ch, nsw = a.nsweep;
     bool wall = false;
@@ -902,6 +925,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         balanced_range(a.col_begin, a.col_end, a.edge_trim, sw, nsw, xa, xb);
     }
     const bool edge = SLAB && (xa < a.wait_lo || xb > a.wait_hi);
+    // an edge wave that signals its stores: write-through in the wall-split walks (the slab builds)
+    const bool wt = (MODE & MODE_SPLIT) && edge && a.done_cnt;
     if constexpr (SLAB)
         if (a.wait_seq && edge) edge_wait(a.wait_seq, a.wait_val, a.wait_err);
     const bool rev = sw & 1;
@@ -914,6 +939,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const unsigned off = (unsigned)(lane * (int)sizeof(T));
         const int et = a.L.ny - 1 - r0;
         const bool owner = lane >= G1 && lane < 64 - G1 && r0 < a.L.ny && (ch == 1 || r0 < OWN1);
+        if constexpr (SLAB) {
+            if (wt) {
+                constexpr int MW = MODE | MODE_WT_STORE;
+                q = rev ? sweepk_walk<T, 1, MW, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0, lw)
+                        : sweepk_walk<T, 1, MW, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0, lw);
+                goto walked;
+            }
+        }
         q = rev ? sweepk_walk<T, 1, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0, lw)
                 : sweepk_walk<T, 1, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0, lw);
     } else if (MODE & MODE_SPLIT) {  // an inner chunk: no wall row within reach of its own rows
@@ -924,6 +957,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const unsigned off = (unsigned)(lane * VS * (int)sizeof(T));
         const int et = a.L.ny - 1 - r0;
         const bool owner = lane >= G && lane < 64 - G && r0 < a.wall_top;
+        if constexpr (SLAB) {
+            if (wt) {
+                constexpr int MW = MODE | MODE_WT_STORE;
+                q = rev ? sweepk_walk<T, VS, MW, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw)
+                        : sweepk_walk<T, VS, MW, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw);
+                goto walked;
+            }
+        }
         q = rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw)
                 : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw);
     } else {
@@ -942,12 +983,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                   : (rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top, lw)
                          : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, bot, top, lw));
     }
+walked:
     if (a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb) {
         const double qs = wave_sum(q);
         if (lane == 0) atomicAdd(a.Q, qs);
     }
     if constexpr (SLAB)
-        if (a.done_cnt && edge) edge_done(a.done_cnt);
+        if (a.done_cnt && edge) edge_done(a.done_cnt, wt);
 }
 
 // Waves of one instantiation resident per CU (256-thread workgroups), and on `cus` CUs (0: all).
@@ -1061,8 +1103,14 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
             // forced to three waves it spills 21 dwords: 0.417 vs 0.323 ms per M f32 launch, profiles/r04/pack)
             constexpr int WPE = sizeof(T) == 4 ? (VS == 2 ? 3 : 4) : (VS == 2 ? 1 : 2);
             if constexpr (sizeof(T) == 4 && VS == 2)
-                if (a.variant & 8)
+                if (a.variant & 8) {
+                    // bit 7 (round 5): two of the three moving populations in LDS, three waves per SIMD
+                    if constexpr (!SLAB)
+                        if (a.variant & 128)
+                            return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PACK | MODE_LDSWIN, K, SLAB, 3>(b, s, stop,
+                                                                                                         start);
                     return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PACK, K, SLAB, 2>(b, s, stop, start);
+                }
             // bit 7 (f64, two cells per lane, with bit 5): the LDS window of the inner chunks
             if constexpr (sizeof(T) == 8 && VS == 2)
                 if ((a.variant & 160) == 160)

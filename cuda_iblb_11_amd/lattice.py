@@ -254,8 +254,11 @@ class Lattice:
         return n.value
 
     # -- timing -----------------------------------------------------------------------------
-    def set_profiling(self, on: bool = True) -> None:
-        self._check(self._lib.iblb_set_profiling(self._h, 1 if on else 0))
+    def set_profiling(self, on=True) -> None:
+        """True / 1: events around every launch; 2: only the deep launches, by their own signals
+        (include/iblb.h iblb_set_profiling); False / 0: off."""
+        mode = 2 if (not isinstance(on, bool) and on == 2) else (1 if on else 0)
+        self._check(self._lib.iblb_set_profiling(self._h, mode))
 
     def timing(self, reset: bool = False) -> dict:
         t = L.Timing()

@@ -236,8 +236,11 @@ int iblb_get_step(iblb_ctx* ctx, long long* steps);
  * at every output iteration (the reference's penalty IB can diverge). */
 int iblb_count_nonfinite(iblb_ctx* ctx, long long* count);
 
-/* Timing: when enabled every collide-stream launch is bracketed by HIP events on the
- * stream it runs on; iblb_get_timing() returns the sums (and resets them if reset). */
+/* Timing: when enabled (1) every collide-stream launch is bracketed by HIP events on the
+ * stream it runs on; iblb_get_timing() returns the sums (and resets them if reset).  enabled = 2:
+ * only the deep (K-iteration) launches are timed, by their own dispatch / completion signals (no
+ * marker packets; the IB band cycle's chain launches run untimed), so that a timed region with IB
+ * keeps its schedule. */
 int iblb_set_profiling(iblb_ctx* ctx, int enabled);
 int iblb_get_timing(iblb_ctx* ctx, iblb_timing* t, int reset);
 /* The same, writing at most `bytes` bytes of the struct (pass sizeof(iblb_timing) of the header the

@@ -21,14 +21,15 @@ rr() {  # tag, ring_reps args (env from the caller)
   echo "$t $(tail -1 $OUT/reps_$t.jsonl | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["nx"], d["ny"], d["precision"], d["median"], d["spread"])')"
 }
 for rep in 1 2; do
-  IBLB_EDGE_FLAG=0 rr noflag 512 4096 f64 --ring || exit 1
-  rr hs 512 4096 f64 --ring || exit 1
-  IBLB_EDGE_TRIM=1 rr trim1 512 4096 f64 --ring || exit 1
-  IBLB_EDGE_TRIM=2 rr trim2 512 4096 f64 --ring || exit 1
-  IBLB_EDGE_FLAG=0 rr noflag32 1024 2048 f32 --ring || exit 1
-  rr hs32 1024 2048 f32 --ring || exit 1
+  IBLB_EDGE_FLAG=2 rr oneway 512 4096 f64 --ring || exit 1
+  IBLB_EDGE_FLAG=2 IBLB_EDGE_TRIM=1 rr oneway_t1 512 4096 f64 --ring || exit 1
+  IBLB_EDGE_FLAG=1 IBLB_EDGE_TRIM=1 rr hs_t1 512 4096 f64 --ring || exit 1
+  IBLB_EDGE_FLAG=1 IBLB_EDGE_TRIM=2 rr hs_t2 512 4096 f64 --ring || exit 1
+  IBLB_EDGE_FLAG=2 rr oneway32 1024 2048 f32 --ring || exit 1
+  IBLB_EDGE_FLAG=1 IBLB_EDGE_TRIM=1 rr hs32_t1 1024 2048 f32 --ring || exit 1
+  IBLB_EDGE_FLAG=1 rr hs32 1024 2048 f32 --ring || exit 1
 done
-rr hs1024 1024 4096 f64 --ring || exit 1
-rr hs2048 2048 4096 f64 --ring || exit 1
+IBLB_EDGE_FLAG=2 rr oneway1024 1024 4096 f64 --ring || exit 1
+IBLB_EDGE_FLAG=2 rr oneway2048 2048 4096 f64 --ring || exit 1
 rr n1 4096 4096 f64 || exit 1
 echo "== done"

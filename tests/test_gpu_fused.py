@@ -622,7 +622,8 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
     equal one-step launches bit for bit, for every cells-per-lane width, sweep length (fixed
     and balanced to whole rounds of waves), variant (f32 variants 2, 3: the wall-row chunks as
     their own sweep family of the three-wave build; 8, 9, 11: the packed two-cell collide, 11 with
-    the wall chunks split off), wave order and walking direction, on
+    the wall chunks split off; 163: f64 LDS window; 139: f32 packed split with two of the three moving
+    populations in LDS, three waves per SIMD), wave order and walking direction, on
     ragged shapes including fewer columns than the K-column reach (periodic images wrap more
     than once).  Calls of 1 + 10K, 2 and 2K - 1 iterations: boot + 10 deep launches, one
     two-iteration launch, then (K >= 4) one launch of depth K - 1 and one of depth K (a call mixes
@@ -646,7 +647,8 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
         for vs in vss:
             for w, var, bal in [(4, 1, 0), (1, 0, 0), (3, 1, 1), (32, 1, 0), (7, 0, 1), (48, 1, 1), (5, 3, 1), (48, 2, 1),
                                 (5, 9, 1), (6, 8, 0), (48, 11, 1), (5, 11, 1), (5, 33, 1), (48, 33, 0), (5, 35, 1), (7, 99, 1), (5, 67, 1),
-                                (6, 35, 0), (4, 11, 0), (3, 3, 0), (5, 107, 1), (6, 107, 0), (5, 163, 1), (48, 163, 0)]:
+                                (6, 35, 0), (4, 11, 0), (3, 3, 0), (5, 107, 1), (6, 107, 0), (5, 163, 1), (48, 163, 0),
+                                (5, 139, 1), (48, 139, 0)]:
                 monkeypatch.setenv("IBLB_DEEP_VS", str(vs))
                 monkeypatch.setenv("IBLB_DEEP_W", str(w))
                 monkeypatch.setenv("IBLB_DEEP_VARIANT", str(var))
