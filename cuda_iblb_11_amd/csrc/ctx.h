@@ -141,6 +141,7 @@ struct iblb_ctx {
     hipEvent_t band_end = nullptr; // recorded on the deep stream at the end of the last band cycle
     char* s_alloc = nullptr;     // two scratch population buffers of the trapezoid (layout of g)
     void* sbuf[2] = {nullptr, nullptr};
+    int probe_level = 0;         // timing probe IBLB_PROBE_LEVEL (lbm_kernels.hip:band_level_kernel)
     int band_merge = 1;          // IBLB_BAND_MERGE: 1 auto, 2 always, 0 never: each level's launch also
                                  // evaluates the next level's force (merged chain)
     bool band_merged = false;    // the installed plan runs the merged chain

@@ -526,6 +526,7 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
         a.c = c->coef;
         a.k = c->kc;
         a.variant = c->variant;
+        a.probe = c->probe_level;
         if (merged) {
             if (j > 0) {  // the force of level j-1, read by the previous launch
                 a.fdclr = fd[(j - 1) % 3];

@@ -886,7 +886,10 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
         HIP_TRY(c, hipEventRecord(c->ev_bnd, c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_int, c->stream));
         c->overlap = env_long("IBLB_OVERLAP", 1) != 0;
-        c->edge_flag = (int)env_long("IBLB_EDGE_FLAG", 1);
+        // one way in f64 (512 x 4096 self ring 0.01502-0.01506 vs 0.01517-0.0152 two-way: the edge waves'
+        // write-through stores cost what the interior's event did), two-way in f32 (1024 x 2048: 0.01094-
+        // 0.0110 vs 0.01125), profiles/r05/hs3
+        c->edge_flag = (int)env_long("IBLB_EDGE_FLAG", is_f64(c) ? 2 : 1);
         c->int_variant = (int)env_long("IBLB_INTERIOR_VARIANT", -1);
         c->edge_trim = (int)std::max(0L, env_long("IBLB_EDGE_TRIM", 0));
         if (!c->sig) {

@@ -346,10 +346,14 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     // f64: the wall split with the level-1 preshift (bits 1, 5: M f64 0.480 vs 0.521 ms per launch,
     // profiles/r04/split64) and the LDS window (bit 7: 163 = 35 | 128; M f64 0.621 vs 0.633 ms per
     // depth-7 launch, 512-column self ring 0.0159 vs 0.0163 ms/iteration, profiles/r04/ldswin)
-    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 163 : 107);
+    // f32, round 5: bit 7 on the packed two-cell walk keeps two of the three moving populations in LDS
+    // (165 VGPRs: three waves per SIMD; 235 = 107 | 128): M f32 0.361 vs 0.387 ms per launch, 320k vs
+    // 300k MLUPS, K5 249k vs 237k (profiles/r05/f32lw); group slabs (one cell per lane) ignore it
+    c->deep_variant = (int)env_long("IBLB_DEEP_VARIANT", f64 ? 163 : 235);
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_merge = (int)env_long("IBLB_BAND_MERGE", 1);
+    c->probe_level = (int)env_long("IBLB_PROBE_LEVEL", 0);
     c->band_par_env = (int)env_long("IBLB_BAND_PAR", 1);
     // cells per lane in a group slab's deep sweeps: f64 two (the wall split needs them: self ring
     // 512 / 1024 / 2048 x 4096 0.0170 / 0.0293 / 0.0531 ms/iteration vs 0.0194 / 0.0343 / 0.0638

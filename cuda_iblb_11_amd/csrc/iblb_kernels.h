@@ -69,6 +69,7 @@ struct FusedArgs {
     const int* n_eps = nullptr;
     double* fdnext = nullptr;
     uint8_t* flnext = nullptr;
+    int probe = 0;  // timing probe IBLB_PROBE_LEVEL (WRONG results): 1 point groups skipped, 2 entry waves skipped
 };
 
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.

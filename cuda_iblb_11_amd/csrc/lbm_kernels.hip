@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
     const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int ew = a.ncols * a.nchl;
     if (gw < ew) {
-        fused_wave<T, V, true, MODE>(a, gw, lane);
+        if (a.probe != 2) fused_wave<T, V, true, MODE>(a, gw, lane);
         return;
     }
     if (gw < ew + a.clr_waves) {
@@ -181,6 +181,7 @@ __global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
         band_clear<V>(a.fdclr, a.flclr, a.fplane, a.L.rows, a.nch, xc, ch, ch * 64 * V + lane * V, lane);
         return;
     }
+    if (a.probe == 1) return;
     const long t = (long)(gw - ew - a.clr_waves) * 64 + lane;
     const int k = (int)(t / NEXT_LANES), n = (int)(t % NEXT_LANES);
     ib_next_group<T>(a, k < a.nns, k, n, 64 * V, reg[threadIdx.x / NEXT_LANES]);

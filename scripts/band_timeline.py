@@ -20,6 +20,12 @@ def main(d):
     deep = [e for e in ev if e[2] == "sweepk_kernel"]
     per = [(b[0] - a[0]) / 1e3 for a, b in zip(deep[-60:], deep[-59:])]
     print(f"cycle (deep start to start): median {statistics.median(per):.1f} us")
+    win = [e for e in ev if deep[-51][0] <= e[0] < deep[-1][0]]
+    kinds = {}
+    for s_, e_, k_, q_ in win:
+        kinds.setdefault(k_, []).append((e_ - s_) / 1e3)
+    print("  median duration per kind over the last 50 cycles: " +
+          ", ".join(f"{k_} {statistics.median(v):.1f} us (x{len(v) / 50:.1f})" for k_, v in sorted(kinds.items())))
     t0 = deep[-4][0]
     for s, e, k, q in ev:
         if deep[-4][0] - 20000 <= s <= deep[-2][0]:

@@ -648,7 +648,7 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
             for w, var, bal in [(4, 1, 0), (1, 0, 0), (3, 1, 1), (32, 1, 0), (7, 0, 1), (48, 1, 1), (5, 3, 1), (48, 2, 1),
                                 (5, 9, 1), (6, 8, 0), (48, 11, 1), (5, 11, 1), (5, 33, 1), (48, 33, 0), (5, 35, 1), (7, 99, 1), (5, 67, 1),
                                 (6, 35, 0), (4, 11, 0), (3, 3, 0), (5, 107, 1), (6, 107, 0), (5, 163, 1), (48, 163, 0),
-                                (5, 139, 1), (48, 139, 0)]:
+                                (5, 139, 1), (48, 139, 0), (6, 235, 1)]:
                 monkeypatch.setenv("IBLB_DEEP_VS", str(vs))
                 monkeypatch.setenv("IBLB_DEEP_W", str(w))
                 monkeypatch.setenv("IBLB_DEEP_VARIANT", str(var))
