@@ -66,7 +66,6 @@ class Timing(C.Structure):
         ("sweepk_launches", C.c_longlong), ("sweepk_ms", C.c_double), ("sweepk_cells", C.c_longlong), ("sweepk_depth", C.c_longlong),
         ("band_cycles", C.c_longlong), ("band_merged_cycles", C.c_longlong), ("band_par_cycles", C.c_longlong),
         ("deep_launches", C.c_longlong), ("deep_iterations", C.c_longlong),
-        ("band_persist_cycles", C.c_longlong),
     ]
 
 

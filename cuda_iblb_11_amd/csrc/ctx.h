@@ -142,10 +142,6 @@ struct iblb_ctx {
     char* s_alloc = nullptr;     // two scratch population buffers of the trapezoid (layout of g)
     void* sbuf[2] = {nullptr, nullptr};
     int probe_level = 0;         // timing probe IBLB_PROBE_LEVEL (lbm_kernels.hip:band_level_kernel)
-    int band_persist = 0;        // IBLB_BAND_PERSIST: the merged chain as one persistent launch (ctx_band.hip)
-    unsigned* chain_bar = nullptr;  // its grid-barrier arrival counter (device) ...
-    unsigned chain_bar_n = 0;       // ... and the arrivals so far
-    long long band_persist_cycles = 0;
     int band_merge = 1;          // IBLB_BAND_MERGE: 1 auto, 2 always, 0 never: each level's launch also
                                  // evaluates the next level's force (merged chain)
     bool band_merged = false;    // the installed plan runs the merged chain

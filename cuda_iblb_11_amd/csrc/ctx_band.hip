@@ -31,8 +31,6 @@
 #include <cstdio>
 #include <cstring>
 
-#include <type_traits>
-
 #include "ctx.h"
 
 namespace iblbh {
@@ -433,15 +431,6 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     return ev_kernel_end(c, ev, EV_SWEEPK, (long long)n * c->ny);
 }
 
-// resident workgroups per CU of the persistent chain kernel (cached)
-template <typename T>
-static int band_chain_bpc(iblb_ctx* c) {
-    static int cached = -1;
-    if (cached < 0) cached = band_chain_blocks_per_cu<T>();
-    (void)c;
-    return cached;
-}
-
 // Columns the force of level j may be spread into (the band trapezoid's [clo, chi)).  Chained
 // levels: the columns level j computes; the last level stores the slab's own columns only, so a
 // force left in a ghost column would never be consumed.  Merged chain: one column less at each
@@ -558,70 +547,7 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
         }
         return a;
     };
-    // The persistent chain (IBLB_BAND_PERSIST, round 5): the merged levels in ONE launch on the chain's
-    // own CUs (a grid barrier between levels, lbm_kernels.hip:band_chain_kernel) instead of one launch per
-    // level; with PAR the last level too.  Only where the chain's stream has CUs of its own (every
-    // workgroup of the grid is resident: the barrier needs them all).
-    int j0 = 0;
-    const int bpc = merged && c->band_persist && c->band_reserve > 0 && bs != ds && K <= CHAIN_MAX_LEVELS &&
-                            (std::is_same<T, double>::value ? c->variant == 5 : c->variant == 3)
-                        ? band_chain_bpc<T>(c)
-                        : 0;
-    if (bpc > 0) {
-        const int nlev = c->band_par ? K : K - 1;
-        ChainArgs<T> ca{};
-        long maxw = 0;
-        for (int j = 0; j < nlev; ++j) {
-            const FusedArgs<T> a = level(j);
-            if (j == 0) ca.base = a;
-            ChainLevel<T>& l = ca.lv[j];
-            l.src = a.src;
-            l.dst = a.dst;
-            l.H = a.H;
-            l.col_begin = a.col_begin;
-            l.ncols = a.ncols;
-            l.nchl = a.nchl;
-            l.store_rows = a.store_rows;
-            l.fdense = a.fdense;
-            l.flags = a.flags;
-            l.fdclr = a.fdclr;
-            l.flclr = a.flclr;
-            l.fkeep = a.fkeep;
-            l.nns = a.nns;
-            l.nG = a.nG;
-            l.n_s = a.n_s;
-            l.n_us = a.n_us;
-            l.n_eps = a.n_eps;
-            l.fdnext = a.fdnext;
-            l.flnext = a.flnext;
-            l.clr_waves = a.clr_waves;
-            l.clr_lo = a.clr_lo;
-            l.clr_hi = a.clr_hi;
-            l.clr_w = a.clr_w;
-            maxw = std::max(maxw, (long)a.ncols * a.nchl + a.clr_waves + ((long)a.nns * NEXT_LANES + 63) / 64);
-        }
-        ca.nlev = nlev;
-        const int blocks = (int)std::max(1L, std::min((maxw + 3) / 4, (long)bpc * c->band_reserve));
-        if (!c->chain_bar) {
-            if ((rc = alloc_zero(c, (void**)&c->chain_bar, 64))) return rc;
-            HIP_TRY(c, hipStreamSynchronize(c->stream));  // (the clear runs on the context's stream)
-            c->chain_bar_n = 0;
-        }
-        if (!c->sig_err) {
-            HIP_TRY(c, hipHostMalloc((void**)&c->sig_err, 64, hipHostMallocCoherent));
-            *c->sig_err = 0;
-        }
-        ca.bar = c->chain_bar;
-        ca.bar0 = c->chain_bar_n;
-        ca.err = c->sig_err;
-        size_t ev = 0;
-        if ((rc = ev_begin(c, &ev, bs))) return rc;
-        HIP_TRY(c, launch_band_chain<T>(ca, blocks, bs, c->band_par ? c->band_end : nullptr));
-        if ((rc = ev_end(c, ev, EV_FUSED, 0, bs))) return rc;
-        c->chain_bar_n += (unsigned)blocks * (unsigned)(nlev - 1);
-        c->band_persist_cycles++;
-        j0 = nlev;
-    }
+    const int j0 = 0;
     for (int j = j0; j < K; ++j) {
         const T* src = j == 0 ? A : S[(j - 1) & 1];
         if (j > 0 && !merged) {  // force^{t+j} from the level below, with the points of iteration t+j-1

@@ -19,7 +19,6 @@ __device__ __forceinline__ int node_x0(float xs) { return (int)nearbyint((double
 // node (x, y) of a point's 3x3 spread, clipped to the lattice (no periodic image, as the
 // reference's cell-centric gather) and to the local columns [xlo, xhi) (default: the slab's own;
 // x_begin: the global column of local column 0 in the caller's image)
-template <int MODE = 0>
 __device__ __forceinline__ void spread_node(const Layout& L, int nx, int x_begin, int x, int y, float xs, float ys,
                                             float Fx, float Fy, int e, double* __restrict__ fd, long fplane,
                                             uint8_t* __restrict__ flags, int nch, int rows_per_chunk, int xlo = 0,
@@ -33,7 +32,7 @@ __device__ __forceinline__ void spread_node(const Layout& L, int nx, int x_begin
     const long o = (long)xc * L.rows + y;
     atomicAdd(fd + o, (double)(Fx * del) * 1. * (double)e);
     atomicAdd(fd + fplane + o, (double)(Fy * del) * 1. * (double)e);
-    st_one<MODE>(flags + (long)xc * nch + y / rows_per_chunk, (uint8_t)1);
+    flags[(long)xc * nch + y / rows_per_chunk] = 1;
 }
 
 // F_s of the group's point from the per-lane node terms, in node order 0..8 (groups of W lanes)
@@ -185,7 +184,7 @@ __device__ __forceinline__ void ib_ghost_group(const T* __restrict__ g, const La
 // rounding of fused_wave (bit for bit the values the level writes), into LDS; then nodes -> F_s ->
 // spread into the next level's force buffer, as ib_ghost_group.
 constexpr int NEXT_RW = 5, NEXT_RH = 7, NEXT_CELLS = NEXT_RW * NEXT_RH;
-// (NEXT_LANES, the lanes per point: iblb_kernels.h)
+constexpr int NEXT_LANES = 32;  // lanes per point: one region cell per lane (5 x 5), a second for 3 lanes (5 x 7)
 
 // this level's post-collision values of cell (xc, y), all nine planes, as fused_wave stores them:
 // the loads (pulls, chunk flag, dense force: zero where no flag is set) ...
@@ -222,7 +221,7 @@ __device__ __forceinline__ void level_cell_collide(const FusedArgs<T>& a, const 
 // slot `reg` (LDS, NEXT_CELLS x 9 values); every lane of the group must call it (shuffles).  The
 // region is 5 x 5 cells (rows y0-2 .. y0+2), one per lane, unless a node crosses the lattice's x
 // edge (the flat-index quirk moves it a row: 5 x 7, rows y0-3 .. y0+3).
-template <typename T, int MODE = 0>
+template <typename T>
 __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, int k, int n, int rows_per_chunk,
                                               T (*reg)[9]) {
 #pragma clang fp contract(off)
@@ -283,7 +282,7 @@ __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, in
         float Fx, Fy;
         fold_terms<NEXT_LANES>(tx, ty, valid, Fx, Fy);
         if (n < 9)
-            spread_node<MODE>(L, G.nx, G.x_begin - m * G.nx, x, y, xs, ys, Fx, Fy, e, a.fdnext, a.fplane, a.flnext, a.nch,
+            spread_node(L, G.nx, G.x_begin - m * G.nx, x, y, xs, ys, Fx, Fy, e, a.fdnext, a.fplane, a.flnext, a.nch,
                         rows_per_chunk, G.clo, G.chi);
         // the region slot is rewritten by the next image: every lane's reads above come first
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -267,7 +267,7 @@ static int reset_cilia_state(iblb_ctx* c) {
     return IBLB_OK;
 }
 
-const char* iblb_version(void) { return "iblb-mi355x 0.5 (gfx950, abi 6)"; }
+const char* iblb_version(void) { return "iblb-mi355x 0.5 (gfx950, abi 5)"; }
 int iblb_abi_version(void) { return IBLB_ABI_VERSION; }
 
 int iblb_device_count(int* n) {
@@ -354,7 +354,6 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_merge = (int)env_long("IBLB_BAND_MERGE", 1);
     c->probe_level = (int)env_long("IBLB_PROBE_LEVEL", 0);
-    c->band_persist = (int)env_long("IBLB_BAND_PERSIST", 0);
     c->band_par_env = (int)env_long("IBLB_BAND_PAR", 1);
     // cells per lane in a group slab's deep sweeps: f64 two (the wall split needs them: self ring
     // 512 / 1024 / 2048 x 4096 0.0170 / 0.0293 / 0.0531 ms/iteration vs 0.0194 / 0.0343 / 0.0638
@@ -442,7 +441,6 @@ void iblb_destroy(iblb_ctx* c) {
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (c->sig) (void)hipFree(c->sig);
-    if (c->chain_bar) (void)hipFree(c->chain_bar);
     if (c->sig_err) (void)hipHostFree(c->sig_err);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->left && c->left->right == c) c->left->right = nullptr;
@@ -784,9 +782,8 @@ int iblb_get_timing_ex(iblb_ctx* c, iblb_timing* out, unsigned long bytes, int r
     t->band_par_cycles = c->band_par_cycles;
     t->deep_launches = c->deep_launches;
     t->deep_iterations = c->deep_iterations;
-    t->band_persist_cycles = c->band_persist_cycles;
     if (reset) {
-        c->band_cycles = c->band_merged_cycles = c->band_par_cycles = c->band_persist_cycles = 0;
+        c->band_cycles = c->band_merged_cycles = c->band_par_cycles = 0;
         c->deep_launches = c->deep_iterations = 0;
         c->fused_ms = c->ib_ms = c->halo_ms = c->sweep_ms = c->sweepk_ms = 0.;
         c->fused_launches = c->fused_cells = c->sweep_launches = c->sweep_cells = 0;

@@ -72,47 +72,6 @@ struct FusedArgs {
     int probe = 0;  // timing probe IBLB_PROBE_LEVEL (WRONG results): 1 point groups skipped, 2 entry waves skipped
 };
 
-// The persistent band chain (lbm_kernels.hip:band_chain_kernel): the merged chain's levels j0 ..
-// j0 + nlev - 1 in ONE launch on CUs of their own, a grid barrier between levels (bounded: after ~2 s a
-// wave sets *err and goes on; the host reports it).  Per level, the FusedArgs fields that change:
-template <typename T>
-struct ChainLevel {
-    const T* src;
-    T* dst;
-    Halo<T> H;
-    int col_begin, ncols, nchl, store_rows;
-    double* fdense;
-    uint8_t* flags;
-    double* fdclr;
-    uint8_t* flclr;
-    int fkeep, nns;
-    IbGhost nG;
-    const float* n_s;
-    const float* n_us;
-    const int* n_eps;
-    double* fdnext;
-    uint8_t* flnext;
-    int clr_waves, clr_lo, clr_hi, clr_w;
-};
-constexpr int CHAIN_MAX_LEVELS = 7;
-// lanes per point of the merged chain's next-level IB (ib_device.h:ib_next_group): one region cell per
-// lane (5 x 5), a second for 3 lanes (5 x 7)
-constexpr int NEXT_LANES = 32;
-template <typename T>
-struct ChainArgs {
-    FusedArgs<T> base;  // the fields every level shares (layout, table, constants, flux, ...)
-    ChainLevel<T> lv[CHAIN_MAX_LEVELS];
-    int nlev;
-    unsigned* bar;      // monotonic arrival counter: barrier b of this launch completes at bar0 + (b+1) * blocks
-    unsigned bar0;
-    unsigned* err;
-};
-template <typename T>
-hipError_t launch_band_chain(const ChainArgs<T>& ca, int blocks, hipStream_t s, hipEvent_t stop);
-// workgroups of band_chain_kernel resident per CU (occupancy API)
-template <typename T>
-int band_chain_blocks_per_cu();
-
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.
 // IB band cycle with its last level beside the deep sweep (and a group slab's boundary sweeps): a patch output region the
 // last level stores and the deep sweep must not: local columns [x0, x1] (inclusive) x rows [y0, y1)

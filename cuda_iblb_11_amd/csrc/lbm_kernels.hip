@@ -14,15 +14,15 @@
 namespace iblb {
 
 // merged band chain: clear the force buffer the previous launch consumed at (column xc, chunk ch)
-template <int V, int MODE = 0>
+template <int V>
 __device__ __forceinline__ void band_clear(double* fd, uint8_t* fl, long fplane, int rows, int nch, int xc, int ch,
                                            int y0, int lane) {
     const long fi = (long)xc * nch + ch;
     if (fl[fi]) {
         double* p = fd + (long)xc * rows + y0;
 #pragma unroll
-        for (int e = 0; e < V; ++e) { st_one<MODE>(p + e, 0.); st_one<MODE>(p + fplane + e, 0.); }
-        if (lane == 0) st_one<MODE>(fl + fi, (uint8_t)0);
+        for (int e = 0; e < V; ++e) { p[e] = 0.; p[fplane + e] = 0.; }
+        if (lane == 0) fl[fi] = 0;
     }
 }
 
@@ -109,11 +109,11 @@ __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, 
         for (int e = 0; e < V; ++e) { fxv[e] = fx[e]; fyv[e] = fy[e]; }
         if (!a.fkeep) {
 #pragma unroll
-            for (int e = 0; e < V; ++e) { st_one<MODE>(fx + e, 0.); st_one<MODE>(fy + e, 0.); }
-            if (lane == 0) st_one<MODE>(a.flags + (long)xc * a.nch + ch, (uint8_t)0);  // only this wave reads this flag
+            for (int e = 0; e < V; ++e) { fx[e] = 0.; fy[e] = 0.; }
+            if (lane == 0) a.flags[(long)xc * a.nch + ch] = 0;  // only this wave reads this flag
         }
     }
-    if (IB && a.flclr) band_clear<V, MODE>(a.fdclr, a.flclr, a.fplane, L.rows, a.nch, xc, ch, y0, lane);
+    if (IB && a.flclr) band_clear<V>(a.fdclr, a.flclr, a.fplane, L.rows, a.nch, xc, ch, y0, lane);
 
     const bool do_flux = a.flux_col >= 0 && xc == a.flux_col;  // (-1: none; ghost column -1 is a real column)
     double q = 0.;
@@ -143,11 +143,9 @@ __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, 
 #pragma unroll
         for (int e = 0; e < V; ++e)
             if (y0 + e >= ya && y0 + e < yb) {
-                st_one<MODE>(dst + e, v0[e]); st_one<MODE>(dst + e + 1 * L.plane, v1[e]);
-                st_one<MODE>(dst + e + 2 * L.plane, v2[e]); st_one<MODE>(dst + e + 3 * L.plane, v3[e]);
-                st_one<MODE>(dst + e + 4 * L.plane, v4[e]); st_one<MODE>(dst + e + 5 * L.plane, v5[e]);
-                st_one<MODE>(dst + e + 6 * L.plane, v6[e]); st_one<MODE>(dst + e + 7 * L.plane, v7[e]);
-                st_one<MODE>(dst + e + 8 * L.plane, v8[e]);
+                dst[e] = v0[e]; dst[e + 1 * L.plane] = v1[e]; dst[e + 2 * L.plane] = v2[e];
+                dst[e + 3 * L.plane] = v3[e]; dst[e + 4 * L.plane] = v4[e]; dst[e + 5 * L.plane] = v5[e];
+                dst[e + 6 * L.plane] = v6[e]; dst[e + 7 * L.plane] = v7[e]; dst[e + 8 * L.plane] = v8[e];
             }
     }
     if (do_flux) {
@@ -188,114 +186,6 @@ __global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
     const int k = (int)(t / NEXT_LANES), n = (int)(t % NEXT_LANES);
     ib_next_group<T>(a, k < a.nns, k, n, 64 * V, reg[threadIdx.x / NEXT_LANES]);
 }
-
-// Grid barrier of the persistent chain (MI355X_MICROARCH.md, inter-workgroup visibility; Guideline
-// 16 R1): every store of a level is write-through (MODE_CHAIN_WT) or a memory-side atomic, drained by
-// each wave's vmcnt(0); then one lane per workgroup adds to a monotonic counter (agent scope), polls
-// it (relaxed agent-scope loads + s_sleep) up to the level's target, and acquires (this CU's L1)
-// before the workgroup's loads of the next level.  Bounded: a workgroup that is not resident (the
-// grid is sized to the chain's CUs) or a lost arrival ends in *err after ~2 s instead of a hang.
-__device__ __forceinline__ void chain_barrier(unsigned* bar, unsigned target, unsigned* err) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        constexpr unsigned LIMIT = 1u << 23;
-        unsigned n = 0;
-        while ((int)(__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-            if (++n > LIMIT) {
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-}
-
-// The merged chain's levels in one launch (ChainArgs, iblb_kernels.h): per level the waves of
-// band_level_kernel — entries, clears, point groups — dealt over the resident grid (grid-stride over
-// the level's wave items), then the grid barrier.  The per-cell arithmetic is band_level_kernel's.
-template <typename T, int V, int MODE>
-__global__ __launch_bounds__(256) void band_chain_kernel(ChainArgs<T> ca) {
-    __shared__ T reg[256 / NEXT_LANES][NEXT_CELLS][9];
-    constexpr int M = MODE | MODE_CHAIN_WT;
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nwv = (int)gridDim.x * 4;
-    for (int j = 0; j < ca.nlev; ++j) {
-        FusedArgs<T> a = ca.base;
-        const ChainLevel<T>& l = ca.lv[j];
-        a.src = l.src;
-        a.dst = l.dst;
-        a.H = l.H;
-        a.col_begin = l.col_begin;
-        a.ncols = l.ncols;
-        a.nchl = l.nchl;
-        a.store_rows = l.store_rows;
-        a.fdense = l.fdense;
-        a.flags = l.flags;
-        a.fdclr = l.fdclr;
-        a.flclr = l.flclr;
-        a.fkeep = l.fkeep;
-        a.nns = l.nns;
-        a.nG = l.nG;
-        a.n_s = l.n_s;
-        a.n_us = l.n_us;
-        a.n_eps = l.n_eps;
-        a.fdnext = l.fdnext;
-        a.flnext = l.flnext;
-        a.clr_waves = l.clr_waves;
-        a.clr_lo = l.clr_lo;
-        a.clr_hi = l.clr_hi;
-        a.clr_w = l.clr_w;
-        const int ew = a.ncols * a.nchl;
-        const int total = ew + a.clr_waves + (a.nns * NEXT_LANES + 63) / 64;
-        for (int gw = (int)blockIdx.x * 4 + wv; gw < total; gw += nwv) {
-            if (gw < ew) {
-                fused_wave<T, V, true, M>(a, gw, lane);
-            } else if (gw < ew + a.clr_waves) {
-                const int c = gw - ew, per = a.clr_w * a.nch;
-                const int r = c < per ? c : c - per;
-                const int xc = (c < per ? a.clr_lo : a.clr_hi) + r / a.nch, ch = r % a.nch;
-                band_clear<V, M>(a.fdclr, a.flclr, a.fplane, a.L.rows, a.nch, xc, ch, ch * 64 * V + lane * V, lane);
-            } else {
-                const long t = (long)(gw - ew - a.clr_waves) * 64 + lane;
-                const int k = (int)(t / NEXT_LANES), n = (int)(t % NEXT_LANES);
-                ib_next_group<T, M>(a, k < a.nns, k, n, 64 * V, reg[threadIdx.x / NEXT_LANES]);
-            }
-        }
-        if (j + 1 < ca.nlev) chain_barrier(ca.bar, ca.bar0 + (unsigned)(j + 1) * gridDim.x, ca.err);
-    }
-}
-
-template <typename T>
-int band_chain_blocks_per_cu() {
-    constexpr int V = vec_of<T>();
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, band_chain_kernel<T, V, sizeof(T) == 8 ? 5 : 3>, 256, 0) !=
-        hipSuccess)
-        return 0;
-    return nb;
-}
-
-template <typename T>
-hipError_t launch_band_chain(const ChainArgs<T>& ca, int blocks, hipStream_t s, hipEvent_t stop) {
-    constexpr int V = vec_of<T>();
-    constexpr int MODE = sizeof(T) == 8 ? 5 : 3;  // the one-step kernels' default variants (IBLB_FUSED_VARIANT)
-    if (ca.base.variant != MODE || blocks <= 0) return hipErrorInvalidValue;
-    if (stop)
-        hipExtLaunchKernelGGL(band_chain_kernel<T, V, MODE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, ca);
-    else
-        band_chain_kernel<T, V, MODE><<<blocks, 256, 0, s>>>(ca);
-    return hipGetLastError();
-}
-template hipError_t launch_band_chain<double>(const ChainArgs<double>&, int, hipStream_t, hipEvent_t);
-template hipError_t launch_band_chain<float>(const ChainArgs<float>&, int, hipStream_t, hipEvent_t);
-template int band_chain_blocks_per_cu<double>();
-template int band_chain_blocks_per_cu<float>();
 
 template <typename T, int MODE>
 hipError_t launch_band_level_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t s, hipEvent_t stop) {

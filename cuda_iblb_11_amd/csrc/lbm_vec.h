@@ -42,17 +42,7 @@ struct Calc<float> { typedef float R; };
 //                  is done in registers (DPP wave_shr / wave_shl by one lane) with one scalar
 //                  load per wave for the element across the chunk edge, instead of
 //                  misaligned 16-B loads
-//   MODE_CHAIN_WT  stores other workgroups of the same launch read after a grid barrier (the
-//                  persistent band chain, lbm_kernels.hip:band_chain_kernel): write-through (sc1), so
-//                  that the barrier needs no L2 write-back (Guideline 16 R1)
-enum { MODE_NT_STORE = 1, MODE_NT_LOAD = 2, MODE_SHIFT = 4, MODE_CHAIN_WT = 1 << 15 };
-
-// scalar store, write-through (agent-scope relaxed atomic store: sc1) under MODE_CHAIN_WT
-template <int MODE, typename U>
-__device__ __forceinline__ void st_one(U* p, U v) {
-    if (MODE & MODE_CHAIN_WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
-}
+enum { MODE_NT_STORE = 1, MODE_NT_LOAD = 2, MODE_SHIFT = 4 };
 
 template <typename T, int V, int MODE>
 __device__ __forceinline__ typename VT<T, V>::type ld_plane(const T* p) {
@@ -63,16 +53,8 @@ __device__ __forceinline__ typename VT<T, V>::type ld_plane(const T* p) {
 template <typename T, int V, int MODE>
 __device__ __forceinline__ void st_plane(T* p, typename VT<T, V>::type v) {
     typedef typename VT<T, V>::type vec;
-    if constexpr ((MODE & MODE_CHAIN_WT) != 0) {
-        static_assert(sizeof(vec) == 16, "16-byte plane rows");
-        typedef unsigned u4 __attribute__((ext_vector_type(4)));
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, 0x7fffffff, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, 0, 0, 16);  // aux 16: sc1
-    } else if (MODE & MODE_NT_STORE) {
-        __builtin_nontemporal_store(v, reinterpret_cast<vec*>(p));
-    } else {
-        sta<T, V>(p, v);
-    }
+    if (MODE & MODE_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<vec*>(p));
+    else sta<T, V>(p, v);
 }
 
 // Move a 32/64-bit value one lane up (dir = +1: lane l receives lane l-1) or down

@@ -55,9 +55,8 @@ extern "C" {
 
 /* ABI version of this header: bumped whenever a struct crossing the ABI changes layout (iblb_config,
  * iblb_timing, iblb_cilia).  5: iblb_timing's band_cycles ... deep_iterations (round 4), the
- * size-checked iblb_get_timing_ex (round 5); 6: iblb_timing.band_persist_cycles.  Compare with
- * iblb_abi_version() at run time. */
-#define IBLB_ABI_VERSION 6
+ * size-checked iblb_get_timing_ex (round 5).  Compare with iblb_abi_version() at run time. */
+#define IBLB_ABI_VERSION 5
 
 /* ---------------------------------------------------------------------------------
  * (1) Reference-shaped kernels.  All pointers are DEVICE pointers.  `stream` is a
@@ -164,8 +163,6 @@ typedef struct iblb_timing {
      * no two-iteration or one-step remainder is left where n allows it (ctx_step.hip:deep_depth) */
     long long deep_launches;
     long long deep_iterations;
-    /* band cycles whose merged chain ran as one persistent launch (IBLB_BAND_PERSIST, round 5) */
-    long long band_persist_cycles;
 } iblb_timing;
 
 /* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */

@@ -106,7 +106,6 @@ def main():
     uid = rccl_unique_id(lib)
     out = [None] * n
     par = [0] * n
-    persist = [0] * n
     gathered = [None] * n
     restarted = [None] * n
     errors = []
@@ -170,7 +169,6 @@ def main():
             if tm["sweepk_launches"] == 0:
                 raise RuntimeError(f"rank {r}: the band cycle did not run")
             par[r] = tm["band_par_cycles"]
-            persist[r] = tm["band_persist_cycles"]
         rs, us = lat.macro()
         out[r] = (xb, xc, rs, us, lat.flux, lat.lagrangian_force() if with_ib else None)  # collective
         gathered[r] = lat.gather_macro(0)  # collective output gather to rank 0
@@ -231,8 +229,6 @@ def main():
         rs_ok = rs_ok and abs(a[4] - b[2]) <= 1e-12 * max(abs(a[4]), 1e-300)
     rs_ok = rs_ok and (d_re == 0.0 if not with_ib else d_re <= 1e-12)
     ok = ok and g_ok and rs_ok
-    if band and os.environ.get("IBLB_BAND_PERSIST") == "1":  # the persistent chain must have run on every rank
-        ok = ok and all(p_ > 0 for p_ in persist)
     d_fs = 0.0
     if with_ib:  # every rank reports the whole F_s (summed over the slabs that hold it)
         d_fs = max(float(np.max(np.abs(o[5] - f1)) / np.max(np.abs(f1))) for o in out)
@@ -244,8 +240,7 @@ def main():
         ok = ok and max(d_oracle.values()) <= (1e-9 if prec == "f64" else 1e-4)
     print(json.dumps({"ok": bool(ok), "exact": exact, "d_rho": d_rho, "d_u": d_u, "d_flux": d_q, "n": n,
                       "gather_ok": g_ok, "restart_ok": bool(rs_ok), "d_restart": d_re, "d_F_s": d_fs,
-                      "with_ib": with_ib, "precision": prec, "d_oracle": d_oracle, "band_par_cycles": par,
-                      "band_persist_cycles": persist}), flush=True)
+                      "with_ib": with_ib, "precision": prec, "d_oracle": d_oracle, "band_par_cycles": par}), flush=True)
     sys.exit(0 if ok else 1)
 
 

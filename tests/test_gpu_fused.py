@@ -859,46 +859,6 @@ def test_ib_band_merged_equals_chained(gpu, oracle, precision, monkeypatch):
     assert abs(runs["2"][2] - runs["0"][2]) <= (1e-11 if precision == "f64" else 1e-5) * max(abs(runs["0"][2]), 1e-30)
 
 
-@pytest.mark.parametrize("precision,par", [("f64", "0"), ("f64", "2"), ("f32", "2")])
-def test_ib_band_persistent_chain(gpu, oracle, precision, par, monkeypatch):
-    """The merged chain as ONE persistent launch (IBLB_BAND_PERSIST=1: the levels on the chain's own CUs
-    with a grid barrier between them, write-through stores, lbm_kernels.hip:band_chain_kernel), with the
-    last level in it (PAR 2) or behind the deep sweep (PAR 0), on the filaments of
-    test_ib_band_merged_equals_chained: equal to the per-level launches up to the arrival order of the
-    spread atomics, and both against the oracle."""
-    nx, ny = 160, 96
-    a, b, c = _line(0.4, 30), _line(nx - 1.3, 24, y0=40.0), _line(70.3, 40, y0=20.0)
-    a[0][0::2] = np.mod(a[0][0::2], nx)
-    pts = tuple(np.concatenate([p, q, r]) for p, q, r in zip(a, b, c))
-    monkeypatch.setenv("IBLB_BAND_MERGE", "2")
-    monkeypatch.setenv("IBLB_BAND_PAR", par)
-    runs = {}
-    for persist in ("1", "0"):
-        monkeypatch.setenv("IBLB_BAND_PERSIST", persist)
-        lat, sim = _static_run(gpu, oracle, nx, ny, 6 * K + 3, pts, chunks=(1, 2 * K + 2, K, 3 * K), precision=precision,
-                               monkeypatch=monkeypatch)
-        tm = lat.timing()
-        runs[persist] = (lat.macro(), lat.force(), lat.flux, tm)
-        check_fields(lat, sim, 1e-9 if precision == "f64" else TOL32)
-        lat.close()
-    for name in ("IBLB_BAND_MERGE", "IBLB_BAND_PAR", "IBLB_BAND_PERSIST"):
-        monkeypatch.delenv(name)
-    assert runs["1"][3]["band_persist_cycles"] >= 5 and runs["0"][3]["band_persist_cycles"] == 0, (runs["1"][3], runs["0"][3])
-    assert runs["1"][3]["band_cycles"] == runs["0"][3]["band_cycles"]
-    (r1, u1), (r0, u0) = runs["1"][0], runs["0"][0]
-    tol = (1e-13, 1e-11) if precision == "f64" else (1e-6, 1e-5)
-    assert rel(r1, r0) <= tol[0] and rel(u1, u0) <= tol[1]
-    assert abs(runs["1"][2] - runs["0"][2]) <= (1e-11 if precision == "f64" else 1e-5) * max(abs(runs["0"][2]), 1e-30)
-
-
-@pytest.mark.parametrize("n,precision", [(2, "f64"), (4, "f32"), (3, "f64")])
-def test_rccl_slab_band_persist(gpu, n, precision, monkeypatch):
-    """The persistent chain on slab groups (mock RCCL, ranks as threads; mode 3: a moving filament
-    across every slab edge, merged chain on every rank): equal to the single slab and the oracle."""
-    monkeypatch.setenv("IBLB_BAND_PERSIST", "1")
-    test_rccl_slab_path_threads(gpu, n, "3", precision, 1, 1, 5, nx=48 * n)
-
-
 def _ulps(a, b):
     """Distance of two float32 arrays in units in the last place."""
     ia = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
