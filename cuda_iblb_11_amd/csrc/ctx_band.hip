@@ -411,6 +411,7 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     // without the LDS window (bit 7): its 144 KB per workgroup would keep the chain's LDS-using
     // kernels off the deep sweep's CUs (K3 136.0 / 137.1k vs 137.5 / 140.9k MLUPS, profiles/r04/ldswin)
     d.variant = sizeof(T) == 8 ? c->deep_variant & ~128 : c->band_own_build ? c->deep_variant : c->deep_variant & 1;
+    if (c->band_deep_variant >= 0) d.variant = c->band_deep_variant;  // (A/B: IBLB_BAND_DEEP_VARIANT)
     d.cus = c->ncu ? (slab ? c->ncu - c->reserved_cus : c->ncu) - std::max(0, c->band_reserve) : 0;
     if (c->band_flux >= 0) {
         d.fskip0 = c->band_fy0;
