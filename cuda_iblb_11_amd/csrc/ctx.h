@@ -76,9 +76,6 @@ struct iblb_ctx {
     int slab_vs = 1;            // cells per lane of a group slab's deep sweeps
     int int_variant = -1;       // deep variant of a group slab's interior sweep (IBLB_INTERIOR_VARIANT; -1: deep_variant)
     int edge_trim = 0;          // slab interiors: first / last sweep narrower by this (IBLB_EDGE_TRIM)
-    int lone_ghost = 0;         // lone slab deep sweeps as ghost-column builds (IBLB_LONE_GHOST)
-    long long gp_t = -1;        // ... the iteration and buffer whose ghost columns hold periodic copies
-    int gp_cur = -1;            //     of its edge columns (-1: none)
     int reserved_cus = 0, ncu = 0;  // CUs kept free of the compute stream (RCCL groups), device CUs
     std::vector<uint32_t> comp_mask;  // the compute stream's CU mask when reserved_cus > 0
     hipStream_t stream = nullptr;

@@ -338,10 +338,7 @@ static int sweep_step(iblb_ctx* c) {
     return IBLB_OK;
 }
 
-// K = d iterations in one launch on a lone slab.  IBLB_LONE_GHOST=1: launched as a ghost-column
-// build (no periodic wrap in the walk's column addressing) whose edge outputs are also stored as the
-// next launch's periodic ghost columns (Sweep2Args::gcopy); the first launch of a chain fills them
-// with two copies.
+// K = d iterations in one launch on a lone slab
 template <typename T>
 static int sweepk_step(iblb_ctx* c, int d) {
     const int W = std::max(1, c->deep_w);
@@ -349,23 +346,13 @@ static int sweepk_step(iblb_ctx* c, int d) {
     Sweep2Args<T> a = sweep_args<T>(c, 0, c->deep_balance ? 0 : W, c->ncol, (c->ncol + W - 1) / W, W);
     a.vs = c->deep_vs;
     a.variant = c->deep_variant;
-    const bool gb = c->lone_ghost && 2 * c->sweep_depth <= c->ncol && d <= c->sweep_depth;
-    int rc;
-    if (gb) {
-        if ((c->gp_t != c->t || c->gp_cur != c->cur) && (rc = fill_ghosts_periodic(c, c->cur, c->sweep_depth, c->stream)))
-            return rc;
-        a.gcopy = c->sweep_depth;
-    }
     size_t ev = 0;
     hipEvent_t e0, e1;  // timing on the launch's own signals (profiling only)
-    if ((rc = ev_kernel(c, &ev, &e0, &e1))) return rc;
-    HIP_TRY(c, launch_sweepk<T>(a, d, gb, c->stream, e1, e0));
+    int rc = ev_kernel(c, &ev, &e0, &e1);
+    if (rc) return rc;
+    HIP_TRY(c, launch_sweepk<T>(a, d, false, c->stream, e1, e0));
     if ((rc = ev_kernel_end(c, ev, EV_SWEEPK, (long long)c->ncol * c->ny))) return rc;
     after_sweep(c, d);
-    if (gb) {
-        c->gp_t = c->t;
-        c->gp_cur = c->cur;
-    }
     c->deep_launches++;
     c->deep_iterations += d;
     return IBLB_OK;

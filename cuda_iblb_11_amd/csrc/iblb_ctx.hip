@@ -355,7 +355,6 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->band_merge = (int)env_long("IBLB_BAND_MERGE", 1);
     c->probe_level = (int)env_long("IBLB_PROBE_LEVEL", 0);
     c->band_deep_variant = (int)env_long("IBLB_BAND_DEEP_VARIANT", -1);
-    c->lone_ghost = (int)env_long("IBLB_LONE_GHOST", 0);
     c->band_par_env = (int)env_long("IBLB_BAND_PAR", 1);
     // cells per lane in a group slab's deep sweeps: f64 two (the wall split needs them: self ring
     // 512 / 1024 / 2048 x 4096 0.0170 / 0.0293 / 0.0531 ms/iteration vs 0.0194 / 0.0343 / 0.0638
@@ -509,7 +508,6 @@ int iblb_set_state(iblb_ctx* c, const double* rho, const double* u, const double
     }
     c->phase = PH_BOOT;
     c->t = 0;
-    c->gp_t = -1;
     c->ib_state = IB_NONE;
     c->ghost = 0;
     c->bnd_w = INT_MAX;
@@ -1017,7 +1015,6 @@ int iblb_load_checkpoint(iblb_ctx* c, const char* path) {
     c->band_dirty = ns > 0 && !c->cilia_on;
     c->t = iv[CK_T];
     c->phase = PH_RUN;
-    c->gp_t = -1;
     c->ghost = 0;
     c->bnd_w = INT_MAX;
     c->ib_state = ib_active(c) ? IB_PENDING : IB_NONE;  // force^t is re-evaluated from g and the points

@@ -118,10 +118,6 @@ struct Sweep2Args {
     unsigned* done_cnt = nullptr;
     int* edge_waves = nullptr;  // host pointer, written by launch_sweepk (not read on the device)
     int edge_trim = 0;          // balanced sweeps: the first and last sweep this many columns narrower
-    // a lone slab run as a ghost-column build (no periodic wrap in the walk): its outputs c < gcopy are
-    // stored again at c + ncol and c >= ncol - gcopy at c - ncol, so that the next launch finds its ghost
-    // columns filled (0: no copies)
-    int gcopy = 0;
     int nskip = 0;       // > 0: the patch output regions below are left to the band's last level,
     SkipBox skip[MAX_SKIP];  // sorted by x0, disjoint in columns (a lone slab's deep sweep, a group slab's interior and boundary sweeps)
 };

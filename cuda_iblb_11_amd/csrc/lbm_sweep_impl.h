@@ -728,14 +728,6 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
             const __amdgpu_buffer_rsrc_t rd = col_rsrc<T>(a.dst + (long)c * a.L.col);
 #pragma unroll
             for (int k = 0; k < 9; ++k) st_rows_buf<T, VS, MODE>(rd, bo.lane, (unsigned)k * bo.plane, out[k]);
-            if constexpr (SLAB) {  // a lone slab's periodic ghost copies (Sweep2Args::gcopy; wave-uniform)
-                if (c < a.gcopy || c >= a.L.ncol - a.gcopy) {
-                    const int c2 = c < a.gcopy ? c + a.L.ncol : c - a.L.ncol;
-                    const __amdgpu_buffer_rsrc_t r2 = col_rsrc<T>(a.dst + (long)c2 * a.L.col);
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) st_rows_buf<T, VS, MODE>(r2, bo.lane, (unsigned)k * bo.plane, out[k]);
-                }
-            }
         }
         if constexpr (LW) {
             int p = 0;

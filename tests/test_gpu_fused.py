@@ -623,8 +623,8 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
     and balanced to whole rounds of waves), variant (f32 variants 2, 3: the wall-row chunks as
     their own sweep family of the three-wave build; 8, 9, 11: the packed two-cell collide, 11 with
     the wall chunks split off; 163: f64 LDS window; 139: f32 packed split with two of the three moving
-    populations in LDS, three waves per SIMD), wave order and walking direction, half of them
-    as ghost-column builds (IBLB_LONE_GHOST=1), on ragged shapes including fewer columns than the K-column reach (periodic images wrap more
+    populations in LDS, three waves per SIMD), wave order and walking direction, on
+    ragged shapes including fewer columns than the K-column reach (periodic images wrap more
     than once).  Calls of 1 + 10K, 2 and 2K - 1 iterations: boot + 10 deep launches, one
     two-iteration launch, then (K >= 4) one launch of depth K - 1 and one of depth K (a call mixes
     the two so that it needs no remainder, ctx_step.hip:deep_depth; K = 3: one deep launch and a
@@ -649,9 +649,6 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
                                 (5, 9, 1), (6, 8, 0), (48, 11, 1), (5, 11, 1), (5, 33, 1), (48, 33, 0), (5, 35, 1), (7, 99, 1), (5, 67, 1),
                                 (6, 35, 0), (4, 11, 0), (3, 3, 0), (5, 107, 1), (6, 107, 0), (5, 163, 1), (48, 163, 0),
                                 (5, 139, 1), (48, 139, 0), (6, 235, 1)]:
-                # every other configuration as a ghost-column build (IBLB_LONE_GHOST: the edge outputs
-                # also stored as the next launch's periodic ghost columns; slabs of >= 2K columns)
-                monkeypatch.setenv("IBLB_LONE_GHOST", str((w + var + bal + vs) % 2))
                 monkeypatch.setenv("IBLB_DEEP_VS", str(vs))
                 monkeypatch.setenv("IBLB_DEEP_W", str(w))
                 monkeypatch.setenv("IBLB_DEEP_VARIANT", str(var))
@@ -669,8 +666,7 @@ def test_sweep_deep_bit_identical(gpu, oracle, precision, depth, monkeypatch):
                                                   float(np.max(np.abs(f - f_ref))))
                 assert abs(lat.flux - q_ref) <= 1e-12 * abs(q_ref), (lat.flux, q_ref)
                 lat.close()
-    for name in ("IBLB_SWEEP_DEPTH", "IBLB_DEEP_VS", "IBLB_DEEP_W", "IBLB_DEEP_VARIANT", "IBLB_DEEP_BALANCE",
-                 "IBLB_LONE_GHOST"):
+    for name in ("IBLB_SWEEP_DEPTH", "IBLB_DEEP_VS", "IBLB_DEEP_W", "IBLB_DEEP_VARIANT", "IBLB_DEEP_BALANCE"):
         monkeypatch.delenv(name)
 
 
