@@ -33,9 +33,9 @@ B="python3 bench.py --no-cpu-baseline"
     -- $B > "$OUT/trace_bench.json" 2> "$OUT/trace.err" || { tail -20 "$OUT/trace.err"; exit 1; }
   find "$OUT/trace" -name "*kernel_stats.csv" -exec head -4 {} \;
   # the depth-7 launches only (the default; a call's K-1 launches carry the same bytes): 70 steps =
-  # ten of them, the kernel named with its template arguments (f64 variant 163 -> mode 785, f32 11 -> 81)
+  # ten of them, the kernel named with its template arguments (f64 variant 163 -> mode 785, f32 235 -> 593)
   for prec in f64 f32; do
-    if [ $prec = f64 ]; then kn="sweepk_kernel<double, 2, 785, 7,"; else kn="sweepk_kernel<float, 2, 81, 7,"; fi
+    if [ $prec = f64 ]; then kn="sweepk_kernel<double, 2, 785, 7,"; else kn="sweepk_kernel<float, 2, 593, 7,"; fi
     for c in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 -s KILL 180 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${c}_$prec" -o pmc \
         -- $B --precision $prec --steps 70 --warmup 7 --prime-seconds 0.3 --no-profile-events > /dev/null 2> "$OUT/pmc_${c}_$prec.err" \
@@ -48,6 +48,18 @@ B="python3 bench.py --no-cpu-baseline"
       --output-format csv -d "$OUT/pmc_valu_$prec" -o pmc \
       -- $B --precision $prec --steps 70 --warmup 7 --prime-seconds 0.3 --no-profile-events > /dev/null 2> "$OUT/pmc_valu_$prec.err" \
       || { tail -20 "$OUT/pmc_valu_$prec.err"; exit 1; }
+  done
+  # the IB configs' deep sweeps inside the band cycle (K3 f64 variant 163 without the window -> mode 273,
+  # K5 f32 235 -> 593)
+  for wl in K3 K5; do
+    if [ $wl = K3 ]; then kn="sweepk_kernel<double, 2, 273, 7,"; key=f64_2048x2048_n1_ib256_sweep7;
+    else kn="sweepk_kernel<float, 2, 593, 7,"; key=f32_8192x2048_n1_ib6144_sweep7; fi
+    for c in FETCH_SIZE WRITE_SIZE; do
+      timeout -k 10 -s KILL 180 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${c}_$wl" -o pmc \
+        -- $B --workload $wl --steps 70 --warmup 7 --prime-seconds 0.3 --no-profile-events > /dev/null 2> "$OUT/pmc_${c}_$wl.err" \
+        || { tail -20 "$OUT/pmc_${c}_$wl.err"; exit 1; }
+    done
+    python3 scripts/pmc_summary.py $key "$OUT/pmc_FETCH_SIZE_$wl" "$OUT/pmc_WRITE_SIZE_$wl" "$OUT/pmc_traffic.json" --kernel "$kn"
   done
   cat "$OUT/pmc_traffic.json"
   echo "== pmc done"
