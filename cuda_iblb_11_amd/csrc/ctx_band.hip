@@ -489,8 +489,8 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
         if ((rc = ib_ghost(c, A, D, clo0, 0, pts_s(c), pts_us(c), pts_eps(c), 0, bs))) return rc;
         if ((rc = ib_ghost(c, A, D, c->ncol, chi0, pts_s(c), pts_us(c), pts_eps(c), 0, bs))) return rc;
     }
-    // the deep sweep first: the chip is full while it runs
-    if ((rc = band_deep<T>(c, K, ds))) return rc;
+    // a lone slab's deep sweep after the level-0 IB (a group slab's: band_step)
+    if (!slab && (rc = band_deep<T>(c, K, ds))) return rc;
     // the launch arguments of level j (merged: its launch also evaluates level j+1's force)
     auto level = [&](int j) {
         const T* src = j == 0 ? A : S[(j - 1) & 1];
@@ -591,11 +591,10 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
 // waits (K3 timeline, profiles/r03k: joining both streams into the context's stream and starting
 // the next cycle from there left 30-40 us of idle chip per cycle); band_join joins them when the
 // run of cycles ends.  A slab of an RCCL group additionally:
-//   comm:    [after the last cycle when it stored edge columns or the halo is deeper than K]
-//            exchange(t, band_x columns) -> [ev_x] -> after the last cycle (it read the columns
-//            the boundary sweeps overwrite) -> boundary sweeps [0, K), [ncol-K, ncol) -> ev_bnd
-//   ds, bs:  after boundary(t-K) (they read its columns); the chain waits for ev_x when its
-//            trapezoids read ghosts and its last level stores edge columns after ev_bnd
+//   bs:      after boundary(t-K) (it wrote columns the cycle reads) and the last cycle: exchange(t,
+//            band_x columns) -> ev_x -> the chain (its trapezoids may read ghost columns)
+//   comm:    ev_x -> boundary sweeps [0, K), [ncol-K, ncol) -> ev_bnd
+//   ds:      after boundary(t-K); a non-PAR last level stores edge columns after ev_bnd
 template <typename T>
 static int band_step(iblb_ctx* c) {
     const int K = c->sweep_depth, D = c->band_d;
@@ -633,20 +632,20 @@ static int band_step(iblb_ctx* c) {
         }
     }
     if (slab) {
-        // everything before this cycle, seen from the comm stream: the previous cycle's end on ds
-        // (chained) or the context's stream
-        // (a PAR cycle ends on two streams: its last level on bs, its deep sweep on ds)
-        hipEvent_t before = chained ? c->band_end : c->ev_pre;
-        const bool before_deep = chained && c->band_prev_par;
+        // a group slab's deep sweep first (round 5: submitted behind the exchange, the boundary sweeps
+        // and the level-0 IB it started late, profiles/r05/lag; a lone slab's streams may be unmasked,
+        // where the chain's level-0 launches go first so that they are not queued behind the deep
+        // sweep's workgroups: band_chain)
+        if ((rc = band_deep<T>(c, K, ds))) return rc;
+        // the exchange on the chain's stream, whose waits above put it after the whole last cycle (it
+        // sends columns the last cycle wrote; the boundary sweeps after it overwrite columns that cycle
+        // read): the chain's level-0 IB follows it in queue order.  On the comm stream the chain waited
+        // for it across queues, and the exchange for the last cycle's end: ~15-20 us per hop on the
+        // cycle's critical path (profiles/r05/df)
         hipStream_t cs = c->comm_stream;
-        if (c->band_x > c->bnd_w) {
-            HIP_TRY(c, hipStreamWaitEvent(cs, before, 0));
-            if (before_deep) HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_deep, 0));
-        }
-        if ((rc = exchange(c, cs, c->band_x))) return rc;
-        if (D > 0) HIP_TRY(c, hipEventRecord(c->ev_x, cs));
-        HIP_TRY(c, hipStreamWaitEvent(cs, before, 0));
-        if (before_deep) HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_deep, 0));
+        if ((rc = exchange(c, bs, c->band_x))) return rc;
+        HIP_TRY(c, hipEventRecord(c->ev_x, bs));
+        HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_x, 0));
         Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
         b.vs = c->slab_vs;
         b.variant = c->deep_variant & ~128;  // beside the chain: no LDS window (above)
@@ -661,10 +660,7 @@ static int band_step(iblb_ctx* c) {
         HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));
     }
-    if (D > 0) {
-        if (slab) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_x, 0));
-        else if ((rc = fill_ghosts_periodic(c, c->cur, D, bs))) return rc;
-    }
+    if (D > 0 && !slab && (rc = fill_ghosts_periodic(c, c->cur, D, bs))) return rc;
     // the end of the cycle (ds: deep sweep and last level, after the chain), recorded by the last
     // level's completion signal: the pinned table slot may be reused once every launch of this cycle
     // has read it, and the next cycle's chain starts after it (a marker packet between the last

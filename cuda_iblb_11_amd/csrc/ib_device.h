@@ -257,6 +257,10 @@ __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, in
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (a.probe == 3) {  // timing probe: the region only (a use the compiler cannot drop)
+            if (reg[n % NEXT_CELLS][0] == (T)12345) a.fdnext[0] = 1.;
+            continue;
+        }
         double tx = 0., ty = 0.;
         bool valid = false;
         const int xn = xl0 + cx(n), x = x0 + cx(n), y = y0 + cy(n);
@@ -281,6 +285,10 @@ __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, in
         }
         float Fx, Fy;
         fold_terms<NEXT_LANES>(tx, ty, valid, Fx, Fy);
+        if (a.probe == 4) {  // timing probe: no spread
+            if (Fx == 12345.f) a.fdnext[0] = 1.;
+            continue;
+        }
         if (n < 9)
             spread_node(L, G.nx, G.x_begin - m * G.nx, x, y, xs, ys, Fx, Fy, e, a.fdnext, a.fplane, a.flnext, a.nch,
                         rows_per_chunk, G.clo, G.chi);

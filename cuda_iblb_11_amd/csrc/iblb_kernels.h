@@ -69,7 +69,8 @@ struct FusedArgs {
     const int* n_eps = nullptr;
     double* fdnext = nullptr;
     uint8_t* flnext = nullptr;
-    int probe = 0;  // timing probe IBLB_PROBE_LEVEL (WRONG results): 1 point groups skipped, 2 entry waves skipped
+    int probe = 0;  // timing probe IBLB_PROBE_LEVEL (WRONG results): 1 point groups skipped, 2 entry waves skipped,
+                    // 3 point groups end after their region, 4 before their spread
 };
 
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.
