@@ -142,6 +142,7 @@ struct iblb_ctx {
     char* s_alloc = nullptr;     // two scratch population buffers of the trapezoid (layout of g)
     void* sbuf[2] = {nullptr, nullptr};
     int probe_level = 0;         // timing probe IBLB_PROBE_LEVEL (lbm_kernels.hip:band_level_kernel)
+    int wrap_split = 1;          // IBLB_WRAP_SPLIT: image groups of their own for points at the x edge (wrap_range)
     int band_deep_variant = -1;  // IBLB_BAND_DEEP_VARIANT: the band cycle's deep variant (-1: band_deep's choice)
     int band_merge = 1;          // IBLB_BAND_MERGE: 1 auto, 2 always, 0 never: each level's launch also
                                  // evaluates the next level's force (merged chain)
@@ -194,9 +195,13 @@ struct iblb_ctx {
     // sweeps signal (IBLB_EDGE_FLAG, default on) instead of the compute queue waiting for ev_bnd
     int edge_flag = 1;  // 1: two-way device handshake, 2: one way (interior waits only), 0: queue waits
     unsigned* sig = nullptr;      // device words: [0] sequence number of the last boundary launch done,
-                                  // [16] edge waves of the slab interiors done (ctx_step.hip:deep_slab_step)
+                                  // [16] edge waves of the slab interiors done (ctx_step.hip:deep_slab_step),
+                                  // [24] band cycles whose exchange landed (ctx_band.hip:band_step)
     unsigned sig_n = 0;           // boundary launches signalled so far (the value of the last one)
     unsigned done_n = 0;          // interior edge waves launched so far (the done word's value once they end)
+    unsigned bx_n = 0;            // band cycles whose exchange the level-0 IB signalled in sig[24] (ctx_band.hip)
+    bool bx_dev = false;          // this band cycle's boundary sweeps wait on sig[24] (set by band_step)
+    bool bnd_deep = false;        // ev_bnd follows the deep sweep of its band cycle too
     bool int_unrec = false;       // the last interior carried no event: ev_int is recorded on demand
     unsigned* sig_err = nullptr;  // host-coherent word: an edge wave's bounded wait timed out
     // profiling
@@ -319,7 +324,7 @@ int fill_ghosts_periodic(iblb_ctx* c, int which, int d, hipStream_t st);
 int ensure_halo(iblb_ctx* c);
 int ensure_force(iblb_ctx* c);
 int ib_ghost(iblb_ctx* c, const void* g, int gc, int clo, int chi, const float* s, const float* us, const int* eps,
-             int part, hipStream_t st);
+             int part, hipStream_t st, unsigned* sig = nullptr, unsigned sig_val = 0);
 int check_ready(iblb_ctx* c);
 int check_wait_err(iblb_ctx* c);  // after a synchronize: did an edge wave's wait time out?
 int prepare_read(iblb_ctx* c);

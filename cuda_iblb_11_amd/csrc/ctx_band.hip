@@ -31,6 +31,8 @@
 #include <cstdio>
 #include <cstring>
 
+#include <functional>
+
 #include "ctx.h"
 
 namespace iblbh {
@@ -432,6 +434,34 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     return ev_kernel_end(c, ev, EV_SWEEPK, (long long)n * c->ny);
 }
 
+// Point indices [*lo, *hi) that may have a periodic image (m = -1 / +1) spreading into the slab's
+// trapezoid columns this cycle: a slab that touches the lattice's x edge, ghost trapezoids (D > 0),
+// points within the trapezoids' reach of that edge at iteration t (the cycle moves them less than a
+// column per iteration; the hint only balances the merged launches' point groups, every image is
+// evaluated either way, band_level_kernel)
+static void wrap_range(const iblb_ctx* c, int* lo, int* hi) {
+    *lo = *hi = 0;
+    const int D = c->band_d, ns = c->ns;
+    if (D <= 0 || ns <= 0 || (c->x_begin != 0 && c->x_begin + c->ncol != c->nx)) return;
+    const float* xy = nullptr;
+    if (c->sch_n > 0) xy = c->sch_x.data() + (size_t)sched_entry(c, c->t) * 2 * ns;
+    else if (c->pts_host.size() >= 2 * (size_t)ns) xy = c->pts_host.data();
+    if (!xy) return;
+    const int margin = D + 2 * c->sweep_depth + 4;
+    int a = INT_MAX, b = -1;
+    for (int k = 0; k < ns; ++k) {
+        const int x0 = (int)std::nearbyint((double)xy[2 * k]);
+        if (x0 < margin || x0 > c->nx - 1 - margin) {
+            a = std::min(a, k);
+            b = k;
+        }
+    }
+    if (b >= 0 && b + 1 - a < ns) {  // (every point: nothing to balance)
+        *lo = a;
+        *hi = b + 1;
+    }
+}
+
 // Columns the force of level j may be spread into (the band trapezoid's [clo, chi)).  Chained
 // levels: the columns level j computes; the last level stores the slab's own columns only, so a
 // force left in a ghost column would never be consumed.  Merged chain: one column less at each
@@ -469,7 +499,8 @@ static void force_clip(const iblb_ctx* c, int j, bool merged, int* clo, int* chi
 // (ev_bnd).  c->band_end is recorded on ds at the end (by the last level's own completion where it
 // launches).
 template <typename T>
-static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool slab, hipStream_t bs, hipStream_t ds) {
+static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool slab, hipStream_t bs, hipStream_t ds,
+                      const std::function<int()>& after_ib0) {
     int rc;
     const int D = c->band_d;
     const bool merged = c->band_merged && c->bf_alloc;
@@ -477,10 +508,16 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
     uint8_t* fl[3] = {c->flags, c->bfl[0], c->bfl[1]};
     int clo0, chi0;
     force_clip(c, 0, merged, &clo0, &chi0);
+    int wlo = 0, whi = 0;
+    if (merged && c->wrap_split) wrap_range(c, &wlo, &whi);
     if (c->ib_state == IB_PENDING) {  // force^t from g^t
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, bs))) return rc;
-        if ((rc = ib_ghost(c, A, D, clo0, chi0, pts_s(c), pts_us(c), pts_eps(c), 0, bs))) return rc;
+        // (bx_dev: its start tells the comm stream's boundary sweeps that the exchange before it landed)
+        if ((rc = ib_ghost(c, A, D, clo0, chi0, pts_s(c), pts_us(c), pts_eps(c), 0, bs, c->bx_dev ? c->sig + 24 : nullptr,
+                           c->bx_n)))
+            return rc;
+        if (c->bx_dev && (rc = after_ib0())) return rc;  // the boundary sweeps, right after their producer
         if ((rc = ev_end(c, ev, EV_IB, 0, bs))) return rc;
         c->ib_state = IB_READY;
     } else if (D > 0) {
@@ -537,6 +574,8 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
                 a.n_eps = pe;
                 a.fdnext = fd[(j + 1) % 3];
                 a.flnext = fl[(j + 1) % 3];
+                a.wlo = wlo;
+                a.whi = whi;
             } else {  // level K-2's force in the ghost columns it may reach (no own entries there)
                 int clo, chi;
                 force_clip(c, K - 2, true, &clo, &chi);
@@ -617,8 +656,9 @@ static int band_step(iblb_ctx* c) {
     } else if (c->band_prev_par) {
         // the last cycle's deep sweep (ds) and last level (bs) wrote disjoint parts of g^t; each stream
         // waits for the other's: the chain reads g^t, the deep sweep reads it and overwrites the
-        // buffer the last cycle's chain read
-        HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_deep, 0));
+        // buffer the last cycle's chain read (a group slab's ev_bnd follows that deep sweep too: one
+        // barrier packet on the chain's queue instead of two, each ~5 us on the cycle's critical path)
+        if (!(slab && c->bnd_deep)) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_deep, 0));
         HIP_TRY(c, hipStreamWaitEvent(ds, c->band_end, 0));
         if (slab) {  // boundary(t-K) wrote columns both read
             HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_bnd, 0));
@@ -631,21 +671,10 @@ static int band_step(iblb_ctx* c) {
             HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_bnd, 0));
         }
     }
-    if (slab) {
-        // a group slab's deep sweep first (round 5: submitted behind the exchange, the boundary sweeps
-        // and the level-0 IB it started late, profiles/r05/lag; a lone slab's streams may be unmasked,
-        // where the chain's level-0 launches go first so that they are not queued behind the deep
-        // sweep's workgroups: band_chain)
-        if ((rc = band_deep<T>(c, K, ds))) return rc;
-        // the exchange on the chain's stream, whose waits above put it after the whole last cycle (it
-        // sends columns the last cycle wrote; the boundary sweeps after it overwrite columns that cycle
-        // read): the chain's level-0 IB follows it in queue order.  On the comm stream the chain waited
-        // for it across queues, and the exchange for the last cycle's end: ~15-20 us per hop on the
-        // cycle's critical path (profiles/r05/df)
-        hipStream_t cs = c->comm_stream;
-        if ((rc = exchange(c, bs, c->band_x))) return rc;
-        HIP_TRY(c, hipEventRecord(c->ev_x, bs));
-        HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_x, 0));
+    hipStream_t cs = c->comm_stream;
+    // a group slab's boundary sweeps [0, K), [ncol-K, ncol) on the comm stream; ev_bnd follows them and
+    // (PAR) this cycle's deep sweep
+    auto boundary = [&]() -> int {
         Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
         b.vs = c->slab_vs;
         b.variant = c->deep_variant & ~128;  // beside the chain: no LDS window (above)
@@ -657,8 +686,44 @@ static int band_step(iblb_ctx* c) {
             b.nskip = (int)c->band_skip.size();
             std::copy(c->band_skip.begin(), c->band_skip.end(), b.skip);
         }
+        if (c->bx_dev) {  // every wave polls the word the level-0 IB sets when it starts (bounded)
+            b.wait_seq = c->sig + 24;
+            b.wait_val = c->bx_n;
+            b.wait_lo = INT_MAX;
+            b.wait_hi = INT_MAX;
+            b.wait_err = c->sig_err;
+        }
         HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));
+        c->bnd_deep = c->band_par;
+        if (c->bnd_deep) HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_deep, 0));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));
+        return IBLB_OK;
+    };
+    c->bx_dev = false;
+    if (slab) {
+        // a group slab's deep sweep first (round 5: submitted behind the exchange, the boundary sweeps
+        // and the level-0 IB it started late, profiles/r05/lag; a lone slab's streams may be unmasked,
+        // where the chain's level-0 launches go first so that they are not queued behind the deep
+        // sweep's workgroups: band_chain)
+        if ((rc = band_deep<T>(c, K, ds))) return rc;
+        // the exchange on the chain's stream, whose waits above put it after the whole last cycle (it
+        // sends columns the last cycle wrote; the boundary sweeps after it overwrite columns that cycle
+        // read): the chain's level-0 IB follows it in queue order.  On the comm stream the chain waited
+        // for it across queues, and the exchange for the last cycle's end: ~15-20 us per hop on the
+        // cycle's critical path (profiles/r05/df)
+        if ((rc = exchange(c, bs, c->band_x))) return rc;
+        // the boundary sweeps need the exchange: with the device words (PAR, reserved CUs, a level-0 IB
+        // over the points) the level-0 IB's first lane signals it when the kernel starts and the boundary
+        // sweeps, submitted after it, poll -- no marker packet between the exchange and the level-0 IB
+        c->bx_dev = ov && c->sig && c->reserved_cus > 0 && c->edge_flag && c->band_par && c->ib_state == IB_PENDING &&
+                    c->ns > 0;
+        if (c->bx_dev) {
+            ++c->bx_n;
+        } else {
+            HIP_TRY(c, hipEventRecord(c->ev_x, bs));
+            HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_x, 0));
+            if ((rc = boundary())) return rc;
+        }
     }
     if (D > 0 && !slab && (rc = fill_ghosts_periodic(c, c->cur, D, bs))) return rc;
     // the end of the cycle (ds: deep sweep and last level, after the chain), recorded by the last
@@ -666,7 +731,8 @@ static int band_step(iblb_ctx* c) {
     // has read it, and the next cycle's chain starts after it (a marker packet between the last
     // level and the next deep sweep left ~7 us of idle queue per cycle, profiles/r03ch2)
     c->band_end = c->band_pin_ev[c->band_pin_cur];  // (the waits above took the previous cycle's)
-    if ((rc = band_chain<T>(c, K, A, B, S, slab, bs, ds))) return rc;
+    // (bx_dev: the boundary sweeps are submitted right after the kernel they wait for)
+    if ((rc = band_chain<T>(c, K, A, B, S, slab, bs, ds, boundary))) return rc;
     c->band_prev_par = c->band_par;
     c->band_cycles++;
     if (c->band_merged && c->bf_alloc) c->band_merged_cycles++;

@@ -22,7 +22,7 @@ __device__ __forceinline__ int node_x0(float xs) { return (int)nearbyint((double
 __device__ __forceinline__ void spread_node(const Layout& L, int nx, int x_begin, int x, int y, float xs, float ys,
                                             float Fx, float Fy, int e, double* __restrict__ fd, long fplane,
                                             uint8_t* __restrict__ flags, int nch, int rows_per_chunk, int xlo = 0,
-                                            int xhi = -1) {
+                                            int xhi = -1, int probe = 0) {
 #pragma clang fp contract(off)
     if (e == 0 || x < 0 || x >= nx || y < 0 || y >= L.ny) return;
     const int xc = x - x_begin;
@@ -30,9 +30,14 @@ __device__ __forceinline__ void spread_node(const Layout& L, int nx, int x_begin
     const float del = d_delta(xs, ys, x, y);
     if (del == 0.f) return;
     const long o = (long)xc * L.rows + y;
-    atomicAdd(fd + o, (double)(Fx * del) * 1. * (double)e);
-    atomicAdd(fd + fplane + o, (double)(Fy * del) * 1. * (double)e);
-    flags[(long)xc * nch + y / rows_per_chunk] = 1;
+    if (probe == 5) {  // timing probe (wrong results): plain stores
+        fd[o] = (double)(Fx * del) * 1. * (double)e;
+        fd[fplane + o] = (double)(Fy * del) * 1. * (double)e;
+    } else {
+        atomicAdd(fd + o, (double)(Fx * del) * 1. * (double)e);
+        atomicAdd(fd + fplane + o, (double)(Fy * del) * 1. * (double)e);
+    }
+    if (probe != 6) flags[(long)xc * nch + y / rows_per_chunk] = 1;  // (6: timing probe, no flag)
 }
 
 // F_s of the group's point from the per-lane node terms, in node order 0..8 (groups of W lanes)
@@ -223,7 +228,7 @@ __device__ __forceinline__ void level_cell_collide(const FusedArgs<T>& a, const 
 // edge (the flat-index quirk moves it a row: 5 x 7, rows y0-3 .. y0+3).
 template <typename T>
 __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, int k, int n, int rows_per_chunk,
-                                              T (*reg)[9]) {
+                                              T (*reg)[9], int imgs = 3) {
 #pragma clang fp contract(off)
     const IbGhost& G = a.nG;
     const Layout& L = a.L;
@@ -240,8 +245,8 @@ __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, in
     const int ry0 = quirk ? y0 - 3 : y0 - 2, ncell = NEXT_RW * (quirk ? NEXT_RH : NEXT_RH - 2);
     for (int m = -1; m <= 1; ++m) {
         const int xl0 = x0 - G.x_begin + m * G.nx;
-        // group-uniform: does this image spread into [clo, chi)?
-        const bool img = pt && xl0 + 1 >= G.clo && xl0 - 1 < G.chi;
+        // group-uniform: does this image spread into [clo, chi)?  (imgs: bit 0 image 0, bit 1 the others)
+        const bool img = pt && (imgs >> (m != 0) & 1) && xl0 + 1 >= G.clo && xl0 - 1 < G.chi;
         if (!img) continue;
         // the region: this level's values of columns xl0-2 .. xl0+2 (cells whose own pulls stay inside
         // the buffer and rows inside the lattice; the others are never read below)
@@ -291,7 +296,7 @@ __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, in
         }
         if (n < 9)
             spread_node(L, G.nx, G.x_begin - m * G.nx, x, y, xs, ys, Fx, Fy, e, a.fdnext, a.fplane, a.flnext, a.nch,
-                        rows_per_chunk, G.clo, G.chi);
+                        rows_per_chunk, G.clo, G.chi, a.probe);
         // the region slot is rewritten by the next image: every lane's reads above come first
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

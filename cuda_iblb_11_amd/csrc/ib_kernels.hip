@@ -49,6 +49,7 @@ __global__ __launch_bounds__(256) void ib_ghost_kernel(const T* __restrict__ g, 
                                                        double* __restrict__ fd, long fplane,
                                                        uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
     const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (G.sig && tid == 0) __hip_atomic_store(G.sig, G.sig_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int k = (int)(tid / LANES_PER_POINT), n = (int)(tid % LANES_PER_POINT);
     ib_ghost_group<T>(g, L, G, k < ns, k, n, s, u_s, eps, F_s, fd, fplane, flags, nch, rows_per_chunk);
 }

@@ -18,6 +18,10 @@ struct IbGhost {
     int gc;        // ghost columns holding valid data (node pulls outside are skipped)
     int clo, chi;  // local columns that receive force
     int part;
+    // the launch's first lane stores sig_val to *sig (agent scope) when the kernel starts: the kernels
+    // before it in its stream are complete (the IB band cycle's exchange, ctx_band.hip)
+    unsigned* sig = nullptr;
+    unsigned sig_val = 0;
 };
 
 template <typename T>
@@ -69,8 +73,13 @@ struct FusedArgs {
     const int* n_eps = nullptr;
     double* fdnext = nullptr;
     uint8_t* flnext = nullptr;
+    // points [wlo, whi): their periodic images (m = -1, +1) are evaluated by groups of their own after
+    // the nns point groups, whose groups then take image m = 0 only (a point at the lattice's x edge
+    // has two images in a slab touching that edge, which one group would walk one after the other)
+    int wlo = 0, whi = 0;
     int probe = 0;  // timing probe IBLB_PROBE_LEVEL (WRONG results): 1 point groups skipped, 2 entry waves skipped,
-                    // 3 point groups end after their region, 4 before their spread
+                    // 3 point groups end after their region, 4 before their spread, 5 spread
+                    // with plain stores, 6 spread without chunk flags
 };
 
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.

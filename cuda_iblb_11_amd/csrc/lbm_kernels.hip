@@ -183,8 +183,13 @@ __global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
     }
     if (a.probe == 1) return;
     const long t = (long)(gw - ew - a.clr_waves) * 64 + lane;
-    const int k = (int)(t / NEXT_LANES), n = (int)(t % NEXT_LANES);
-    ib_next_group<T>(a, k < a.nns, k, n, 64 * V, reg[threadIdx.x / NEXT_LANES]);
+    const int gi = (int)(t / NEXT_LANES), n = (int)(t % NEXT_LANES);
+    // group gi < nns: point gi (image 0 only when it lies in [wlo, whi)); then one group per point of
+    // [wlo, whi) for its images -1 and +1 (FusedArgs::wlo)
+    const bool main = gi < a.nns;
+    const int k = main ? gi : a.wlo + (gi - a.nns);
+    const int imgs = main ? (k >= a.wlo && k < a.whi ? 1 : 3) : 2;  // bit 0: m = 0, bit 1: m = +-1
+    ib_next_group<T>(a, main || k < a.whi, k, n, 64 * V, reg[threadIdx.x / NEXT_LANES], imgs);
 }
 
 template <typename T, int MODE>
@@ -217,7 +222,7 @@ hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t
 template <typename T>
 hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s, hipEvent_t stop) {
     long waves = (long)a.ncols * (a.row_tab ? a.nchl : a.nch);
-    if (a.row_tab) waves += a.clr_waves + ((long)a.nns * NEXT_LANES + 63) / 64;
+    if (a.row_tab) waves += a.clr_waves + ((long)(a.nns + std::max(0, a.whi - a.wlo)) * NEXT_LANES + 63) / 64;
     if (waves <= 0) return hipSuccess;
     if (a.row_tab && (a.nns > 0 || a.clr_waves > 0) && !a.flags) return hipErrorInvalidValue;
     const unsigned blocks = (unsigned)((waves + 3) / 4);

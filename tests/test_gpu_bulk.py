@@ -328,18 +328,23 @@ def test_band_streams_keep_the_context_stream(gpu, monkeypatch):
     assert rel(r1, r2) <= 1e-13 and rel(u1, u2) <= 1e-12
 
 
+@pytest.mark.parametrize("par", ["2", "0"])
 @pytest.mark.parametrize("precision,where", [("f64", "inside"), ("f32", "inside"), ("f64", "edge"), ("f32", "edge")])
-def test_rccl_self_ring_ib_band_cycle(gpu, monkeypatch, precision, where):
+def test_rccl_self_ring_ib_band_cycle(gpu, monkeypatch, precision, where, par):
     """The IB band cycle of a slab group over REAL RCCL (one rank, its own neighbour): moving
     filaments, points given ahead, bulk calls with readers between them; equals the lone slab up to
     the spread atomics' order.  inside: the filaments stay inside the slab; edge: they cross the
-    slab edge (x = 0): the cycle's exchange carries 3K ghost columns and the trapezoids advance them."""
+    slab edge (x = 0): the cycle's exchange carries 3K ghost columns and the trapezoids advance them.
+    par 2: the last level beside the deep sweep, the boundary sweeps told by the level-0 IB that the
+    exchange (on the chain's stream) landed (device word, ctx_band.hip:band_step); 0: the last level
+    behind the deep sweep, the boundary sweeps after the exchange's event."""
     from cuda_iblb_11_amd import workloads as W
     monkeypatch.setenv("IBLB_RCCL_SELF", "1")
+    monkeypatch.setenv("IBLB_BAND_PAR", par)
     nx, ny = 256, 128
-    pts = _swaying(nx, n_fil=2, pts=40) if where == "inside" else _crossing(nx)
+    pts = _swaying(nx, n_fil=2, pts=40) if where == "inside" else _crossing(nx, mid=True)
     rho, u = W.perturbed_state(nx, ny, 17)
-    kw = dict(precision=precision, body_force=(1e-6, 0.0), max_points=80)
+    kw = dict(precision=precision, body_force=(1e-6, 0.0), max_points=120)
     ref = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)
     ring = gpu.Lattice(nx, ny, W.TAU, W.TAU2, **kw)
     ref.set_state(rho, u)
@@ -356,18 +361,22 @@ def test_rccl_self_ring_ib_band_cycle(gpu, monkeypatch, precision, where):
         r2, u2 = ring.macro()
         tol = 1e-12 if precision == "f64" else 1e-5
         assert rel(r2, r1) <= tol and rel(u2, u1) <= tol, n
-    assert ring.timing()["sweepk_launches"] >= 4
+    tm = ring.timing()
+    assert tm["sweepk_launches"] >= 4 and tm["band_cycles"] >= 4, tm
+    assert (tm["band_par_cycles"] == tm["band_cycles"]) == (par == "2"), tm
     assert abs(ring.flux - ref.flux) <= 1e-11 * abs(ref.flux)
     ring.close()
 
 
-def _crossing(nx, pts=40, period=24):
-    """Two filaments that sway across x = 0 / XDIM (wrapped into [0, XDIM) like boundary_check,
-    main.cu:193-196) and one near XDIM-1."""
+def _crossing(nx, pts=40, period=24, mid=False):
+    """A filament that sways across x = 0 / XDIM (wrapped into [0, XDIM) like boundary_check,
+    main.cu:193-196) and one near XDIM-1; mid: a third one in the middle first, so that the points
+    near the x edge are a strict index range (the merged launches' image groups, FusedArgs::wlo)."""
     def points(it):
         k = np.arange(pts)
         s_all, u_all = [], []
-        for m, (x0, y0) in enumerate(((0.3, 2.0), (nx - 2.2, 50.0))):
+        starts = ((nx / 2 + 0.4, 30.0),) if mid else ()
+        for m, (x0, y0) in enumerate(starts + ((0.3, 2.0), (nx - 2.2, 50.0))):
             ph = 2 * np.pi * (it + 5 * m) / period
             s = np.empty(2 * pts, np.float32)
             s[0::2] = np.mod(x0 + 2.0 * (k / pts) * np.sin(ph), nx)
@@ -386,7 +395,7 @@ def test_moving_points_across_x0(gpu, oracle, precision, monkeypatch):
     """Filaments swaying across x = 0 through the lone slab's band cycle (ghost columns filled by
     periodic copies every cycle), against the oracle."""
     nx, ny = 256, 128
-    lat, sim = moving_run(gpu, oracle, nx, ny, _crossing(nx), CHUNKS, precision=precision,
+    lat, sim = moving_run(gpu, oracle, nx, ny, _crossing(nx, mid=True), CHUNKS, precision=precision,
                           monkeypatch=monkeypatch, readers=True)
     assert lat.timing()["sweepk_launches"] >= 6
     r = fields(lat, sim)
