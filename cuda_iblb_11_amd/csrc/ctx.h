@@ -324,7 +324,7 @@ int fill_ghosts_periodic(iblb_ctx* c, int which, int d, hipStream_t st);
 int ensure_halo(iblb_ctx* c);
 int ensure_force(iblb_ctx* c);
 int ib_ghost(iblb_ctx* c, const void* g, int gc, int clo, int chi, const float* s, const float* us, const int* eps,
-             int part, hipStream_t st, unsigned* sig = nullptr, unsigned sig_val = 0);
+             int part, hipStream_t st, unsigned* sig = nullptr, unsigned sig_val = 0, int wlo = 0, int whi = 0);
 int check_ready(iblb_ctx* c);
 int check_wait_err(iblb_ctx* c);  // after a synchronize: did an edge wave's wait time out?
 int prepare_read(iblb_ctx* c);

@@ -509,15 +509,14 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
     int clo0, chi0;
     force_clip(c, 0, merged, &clo0, &chi0);
     int wlo = 0, whi = 0;
-    if (merged && c->wrap_split) wrap_range(c, &wlo, &whi);
+    if (c->wrap_split) wrap_range(c, &wlo, &whi);
     if (c->ib_state == IB_PENDING) {  // force^t from g^t
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, bs))) return rc;
         // (bx_dev: its start tells the comm stream's boundary sweeps that the exchange before it landed)
         if ((rc = ib_ghost(c, A, D, clo0, chi0, pts_s(c), pts_us(c), pts_eps(c), 0, bs, c->bx_dev ? c->sig + 24 : nullptr,
-                           c->bx_n)))
+                           c->bx_n, wlo, whi)))
             return rc;
-        if (c->bx_dev && (rc = after_ib0())) return rc;  // the boundary sweeps, right after their producer
         if ((rc = ev_end(c, ev, EV_IB, 0, bs))) return rc;
         c->ib_state = IB_READY;
     } else if (D > 0) {
@@ -587,8 +586,8 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
         }
         return a;
     };
-    const int j0 = 0;
-    for (int j = j0; j < K; ++j) {
+    bool bnd_sub = false;  // the boundary sweeps submitted (bx_dev)
+    for (int j = 0; j < K; ++j) {
         const T* src = j == 0 ? A : S[(j - 1) & 1];
         if (j > 0 && !merged) {  // force^{t+j} from the level below, with the points of iteration t+j-1
             const float *ps, *pus;
@@ -598,7 +597,7 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
             force_clip(c, j, false, &clo, &chi);
             size_t ev = 0;
             if ((rc = ev_begin(c, &ev, bs))) return rc;
-            if ((rc = ib_ghost(c, src, D, clo, chi, ps, pus, pe, 0, bs))) return rc;
+            if ((rc = ib_ghost(c, src, D, clo, chi, ps, pus, pe, 0, bs, nullptr, 0, wlo, whi))) return rc;
             if ((rc = ev_end(c, ev, EV_IB, 0, bs))) return rc;
         }
         const FusedArgs<T> a = level(j);
@@ -619,7 +618,14 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
         if ((rc = ev_begin(c, &ev, ls))) return rc;
         HIP_TRY(c, launch_fused<T>(a, ls, j == K - 1 ? c->band_end : nullptr));
         if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * a.nchl * 64 * c->V, ls))) return rc;
+        // bx_dev: the boundary sweeps after their producer (the level-0 IB) and after the first level,
+        // so that their host-side submission does not delay the chain's first launches
+        if (j == 0 && c->bx_dev && !bnd_sub) {
+            bnd_sub = true;
+            if ((rc = after_ib0())) return rc;
+        }
     }
+    if (c->bx_dev && !bnd_sub && (rc = after_ib0())) return rc;  // (no level-0 launch)
     return IBLB_OK;
 }
 

@@ -91,8 +91,8 @@ int ensure_halo(iblb_ctx* c) {
 
 // ---- immersed boundary ------------------------------------------------------------------------
 int ib_ghost(iblb_ctx* c, const void* g, int gc, int clo, int chi, const float* s, const float* us, const int* eps,
-             int part, hipStream_t st, unsigned* sig, unsigned sig_val) {
-    IbGhost G{c->nx, c->x_begin, gc, clo, chi, part, sig, sig_val};
+             int part, hipStream_t st, unsigned* sig, unsigned sig_val, int wlo, int whi) {
+    IbGhost G{c->nx, c->x_begin, gc, clo, chi, part, sig, sig_val, wlo, whi};
     if (is_f64(c))
         HIP_TRY(c, launch_ib_ghost<double>((const double*)g, c->L, G, c->ns, s, us, eps, c->d_Fs, c->fdense, c->fplane,
                                            c->flags, c->nch, 64 * c->V, st));

@@ -127,7 +127,7 @@ __device__ __forceinline__ void ib_ghost_group(const T* __restrict__ g, const La
                                                int k, int n, const float* __restrict__ s,
                                                const float* __restrict__ u_s, const int* __restrict__ eps,
                                                float* __restrict__ F_s, double* __restrict__ fd, long fplane,
-                                               uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
+                                               uint8_t* __restrict__ flags, int nch, int rows_per_chunk, int imgs = 3) {
 #pragma clang fp contract(off)
     float xs = 0.f, ys = 0.f;
     int x0 = 0, y0 = 0;
@@ -142,7 +142,7 @@ __device__ __forceinline__ void ib_ghost_group(const T* __restrict__ g, const La
         const int xl = x0 - G.x_begin;
         const bool inner = xl >= 2 && xl <= L.ncol - 3;
         go = G.part == 0 || (G.part == 1) == inner;
-        if (go && !own && n == 0) {  // another slab reports this point's F_s
+        if (go && !own && n == 0 && (imgs & 1)) {  // another slab reports this point's F_s
             F_s[2 * k + 0] = 0.f;
             F_s[2 * k + 1] = 0.f;
         }
@@ -151,7 +151,7 @@ __device__ __forceinline__ void ib_ghost_group(const T* __restrict__ g, const La
     for (int m = -1; m <= 1; ++m) {
         const int xl0 = x0 - G.x_begin + m * G.nx;
         // group-uniform: does this image spread into [clo, chi)?
-        const bool img = go && (G.part != 1 || m == 0) && xl0 + 1 >= G.clo && xl0 - 1 < G.chi;
+        const bool img = go && (imgs >> (m != 0) & 1) && (G.part != 1 || m == 0) && xl0 + 1 >= G.clo && xl0 - 1 < G.chi;
         if (!img) continue;
         double tx = 0., ty = 0.;
         bool valid = false;

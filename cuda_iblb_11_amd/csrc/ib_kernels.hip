@@ -50,8 +50,13 @@ __global__ __launch_bounds__(256) void ib_ghost_kernel(const T* __restrict__ g, 
                                                        uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
     const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (G.sig && tid == 0) __hip_atomic_store(G.sig, G.sig_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int k = (int)(tid / LANES_PER_POINT), n = (int)(tid % LANES_PER_POINT);
-    ib_ghost_group<T>(g, L, G, k < ns, k, n, s, u_s, eps, F_s, fd, fplane, flags, nch, rows_per_chunk);
+    // group gi < ns: point gi (image 0 only when it lies in [wlo, whi)); then one group per point of
+    // [wlo, whi) for its images -1 and +1 (IbGhost::wlo)
+    const int gi = (int)(tid / LANES_PER_POINT), n = (int)(tid % LANES_PER_POINT);
+    const bool main = gi < ns;
+    const int k = main ? gi : G.wlo + (gi - ns);
+    const int imgs = main ? (k >= G.wlo && k < G.whi ? 1 : 3) : 2;
+    ib_ghost_group<T>(g, L, G, main || k < G.whi, k, n, s, u_s, eps, F_s, fd, fplane, flags, nch, rows_per_chunk, imgs);
 }
 
 template <typename T>
@@ -60,7 +65,7 @@ hipError_t launch_ib_ghost(const T* g, Layout L, IbGhost G, int ns, const float*
                            hipStream_t st) {
     if (ns <= 0) return hipSuccess;
     if (G.gc < 0 || G.clo < -G.gc || G.chi > L.ncol + G.gc || G.nx < L.ncol) return hipErrorInvalidValue;
-    const long n = (long)LANES_PER_POINT * ns;
+    const long n = (long)LANES_PER_POINT * (ns + std::max(0, G.whi - G.wlo));
     ib_ghost_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(g, L, G, ns, s, u_s, eps, F_s, fdense, fplane,
                                                                      flags, nch, rows_per_chunk);
     return hipGetLastError();

@@ -22,6 +22,9 @@ struct IbGhost {
     // before it in its stream are complete (the IB band cycle's exchange, ctx_band.hip)
     unsigned* sig = nullptr;
     unsigned sig_val = 0;
+    // points [wlo, whi): their images -1 / +1 in groups of their own after the ns point groups (as
+    // FusedArgs::wlo)
+    int wlo = 0, whi = 0;
 };
 
 template <typename T>

@@ -160,36 +160,40 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
                                threadIdx.x & 63);
 }
 
-// A level of the merged band chain (FusedArgs: fkeep, fdclr, clr_waves, nns): the waves of the
-// table entries (fused_wave), then clr_waves clear-only waves, then the 16-lane point groups of the
-// next level's IB (ib_next_group).  The roles are wave-uniform; the point groups synchronise only
-// within their wave (LDS region per group).
+// A level of the merged band chain (FusedArgs: fkeep, fdclr, clr_waves, nns): the 32-lane point
+// groups of the next level's IB (ib_next_group) first — the launch's longest waves, dispatched before
+// the others — then the waves of the table entries (fused_wave), then clr_waves clear-only waves.  The
+// roles are wave-uniform; the point groups synchronise only within their wave (LDS region per group).
 template <typename T, int V, int MODE>
 __global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
     __shared__ T reg[256 / NEXT_LANES][NEXT_CELLS][9];
     const int lane = threadIdx.x & 63;
     const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    const int ew = a.ncols * a.nchl;
-    if (gw < ew) {
-        if (a.probe != 2) fused_wave<T, V, true, MODE>(a, gw, lane);
+    const int ngroups = a.nns > 0 ? a.nns + max(0, a.whi - a.wlo) : 0;
+    const int pw = (ngroups * NEXT_LANES + 63) / 64;
+    if (gw < pw) {
+        if (a.probe == 1) return;
+        const long t = (long)gw * 64 + lane;
+        const int gi = (int)(t / NEXT_LANES), n = (int)(t % NEXT_LANES);
+        // group gi < nns: point gi (image 0 only when it lies in [wlo, whi)); then one group per point
+        // of [wlo, whi) for its images -1 and +1 (FusedArgs::wlo)
+        const bool main = gi < a.nns;
+        const int k = main ? gi : a.wlo + (gi - a.nns);
+        const int imgs = main ? (k >= a.wlo && k < a.whi ? 1 : 3) : 2;  // bit 0: m = 0, bit 1: m = +-1
+        ib_next_group<T>(a, main || k < a.whi, k, n, 64 * V, reg[threadIdx.x / NEXT_LANES], imgs);
         return;
     }
-    if (gw < ew + a.clr_waves) {
-        const int c = gw - ew, per = a.clr_w * a.nch;
+    const int w = gw - pw, ew = a.ncols * a.nchl;
+    if (w < ew) {
+        if (a.probe != 2) fused_wave<T, V, true, MODE>(a, w, lane);
+        return;
+    }
+    if (w < ew + a.clr_waves) {
+        const int c = w - ew, per = a.clr_w * a.nch;
         const int r = c < per ? c : c - per;
         const int xc = (c < per ? a.clr_lo : a.clr_hi) + r / a.nch, ch = r % a.nch;
         band_clear<V>(a.fdclr, a.flclr, a.fplane, a.L.rows, a.nch, xc, ch, ch * 64 * V + lane * V, lane);
-        return;
     }
-    if (a.probe == 1) return;
-    const long t = (long)(gw - ew - a.clr_waves) * 64 + lane;
-    const int gi = (int)(t / NEXT_LANES), n = (int)(t % NEXT_LANES);
-    // group gi < nns: point gi (image 0 only when it lies in [wlo, whi)); then one group per point of
-    // [wlo, whi) for its images -1 and +1 (FusedArgs::wlo)
-    const bool main = gi < a.nns;
-    const int k = main ? gi : a.wlo + (gi - a.nns);
-    const int imgs = main ? (k >= a.wlo && k < a.whi ? 1 : 3) : 2;  // bit 0: m = 0, bit 1: m = +-1
-    ib_next_group<T>(a, main || k < a.whi, k, n, 64 * V, reg[threadIdx.x / NEXT_LANES], imgs);
 }
 
 template <typename T, int MODE>
@@ -222,7 +226,8 @@ hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t
 template <typename T>
 hipError_t launch_fused(const FusedArgs<T>& a, hipStream_t s, hipEvent_t stop) {
     long waves = (long)a.ncols * (a.row_tab ? a.nchl : a.nch);
-    if (a.row_tab) waves += a.clr_waves + ((long)(a.nns + std::max(0, a.whi - a.wlo)) * NEXT_LANES + 63) / 64;
+    if (a.row_tab && a.nns > 0) waves += ((long)(a.nns + std::max(0, a.whi - a.wlo)) * NEXT_LANES + 63) / 64;
+    if (a.row_tab) waves += a.clr_waves;
     if (waves <= 0) return hipSuccess;
     if (a.row_tab && (a.nns > 0 || a.clr_waves > 0) && !a.flags) return hipErrorInvalidValue;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
