@@ -113,7 +113,7 @@ static int band_streams(iblb_ctx* c, long long band_cols, long long deep_cols) {
     want = env_long("IBLB_BAND_CUS", want);
     if (want == -2 && slab) want = per_xcd;  // a group slab's comm stream owns the reserved CUs
     if (want >= avail) want = 0;
-    c->band_own_build = own_build && want == per_xcd;
+    c->band_own_build = own_build && want > 0;  // (the chain masked to CUs of its own, any count: IBLB_BAND_CUS)
     if (want == c->band_reserve || (c->band_sticky && c->band_st)) return IBLB_OK;
     if ((rc_ = band_join(c))) return rc_;
     HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -13,6 +13,7 @@
 namespace iblb {
 
 constexpr int LANES_PER_POINT = 16;
+constexpr int GHOST_PPW = 7;  // ib_ghost_kernel: points per wave (nine lanes each)
 
 __device__ __forceinline__ int node_x0(float xs) { return (int)nearbyint((double)xs); }
 
@@ -51,6 +52,23 @@ __device__ __forceinline__ void fold_terms(double tx, double ty, bool valid, flo
         const double ax = __shfl(tx, m, W);
         const double ay = __shfl(ty, m, W);
         if (__shfl((int)valid, m, W)) {
+            Fx = (float)((double)Fx + ax);
+            Fy = (float)((double)Fy + ay);
+        }
+    }
+}
+
+// The same fold for a group of nine lanes starting at lane `base` of the wave (ib_ghost_kernel:
+// seven points per wave instead of four)
+__device__ __forceinline__ void fold_terms_at(double tx, double ty, bool valid, int base, float& Fx, float& Fy) {
+#pragma clang fp contract(off)
+    Fx = 0.f;
+    Fy = 0.f;
+#pragma unroll
+    for (int m = 0; m < 9; ++m) {
+        const double ax = __shfl(tx, base + m);
+        const double ay = __shfl(ty, base + m);
+        if (__shfl((int)valid, base + m)) {
             Fx = (float)((double)Fx + ax);
             Fy = (float)((double)Fy + ay);
         }
@@ -127,7 +145,8 @@ __device__ __forceinline__ void ib_ghost_group(const T* __restrict__ g, const La
                                                int k, int n, const float* __restrict__ s,
                                                const float* __restrict__ u_s, const int* __restrict__ eps,
                                                float* __restrict__ F_s, double* __restrict__ fd, long fplane,
-                                               uint8_t* __restrict__ flags, int nch, int rows_per_chunk, int imgs = 3) {
+                                               uint8_t* __restrict__ flags, int nch, int rows_per_chunk, int imgs,
+                                               int base) {
 #pragma clang fp contract(off)
     float xs = 0.f, ys = 0.f;
     int x0 = 0, y0 = 0;
@@ -168,7 +187,7 @@ __device__ __forceinline__ void ib_ghost_group(const T* __restrict__ g, const La
             }
         }
         float Fx, Fy;
-        fold_terms(tx, ty, valid, Fx, Fy);
+        fold_terms_at(tx, ty, valid, base, Fx, Fy);
         if (n == 0 && m == 0 && own) {
             F_s[2 * k + 0] = Fx;
             F_s[2 * k + 1] = Fy;
