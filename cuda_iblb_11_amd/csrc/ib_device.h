@@ -23,7 +23,7 @@ __device__ __forceinline__ int node_x0(float xs) { return (int)nearbyint((double
 __device__ __forceinline__ void spread_node(const Layout& L, int nx, int x_begin, int x, int y, float xs, float ys,
                                             float Fx, float Fy, int e, double* __restrict__ fd, long fplane,
                                             uint8_t* __restrict__ flags, int nch, int rows_per_chunk, int xlo = 0,
-                                            int xhi = -1, int probe = 0) {
+                                            int xhi = -1) {
 #pragma clang fp contract(off)
     if (e == 0 || x < 0 || x >= nx || y < 0 || y >= L.ny) return;
     const int xc = x - x_begin;
@@ -31,14 +31,9 @@ __device__ __forceinline__ void spread_node(const Layout& L, int nx, int x_begin
     const float del = d_delta(xs, ys, x, y);
     if (del == 0.f) return;
     const long o = (long)xc * L.rows + y;
-    if (probe == 5) {  // timing probe (wrong results): plain stores
-        fd[o] = (double)(Fx * del) * 1. * (double)e;
-        fd[fplane + o] = (double)(Fy * del) * 1. * (double)e;
-    } else {
-        atomicAdd(fd + o, (double)(Fx * del) * 1. * (double)e);
-        atomicAdd(fd + fplane + o, (double)(Fy * del) * 1. * (double)e);
-    }
-    if (probe != 6) flags[(long)xc * nch + y / rows_per_chunk] = 1;  // (6: timing probe, no flag)
+    atomicAdd(fd + o, (double)(Fx * del) * 1. * (double)e);
+    atomicAdd(fd + fplane + o, (double)(Fy * del) * 1. * (double)e);
+    flags[(long)xc * nch + y / rows_per_chunk] = 1;
 }
 
 // F_s of the group's point from the per-lane node terms, in node order 0..8 (groups of W lanes)
@@ -315,7 +310,7 @@ __device__ __forceinline__ void ib_next_group(const FusedArgs<T>& a, bool pt, in
         }
         if (n < 9)
             spread_node(L, G.nx, G.x_begin - m * G.nx, x, y, xs, ys, Fx, Fy, e, a.fdnext, a.fplane, a.flnext, a.nch,
-                        rows_per_chunk, G.clo, G.chi, a.probe);
+                        rows_per_chunk, G.clo, G.chi);
         // the region slot is rewritten by the next image: every lane's reads above come first
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

@@ -81,8 +81,8 @@ struct FusedArgs {
     // has two images in a slab touching that edge, which one group would walk one after the other)
     int wlo = 0, whi = 0;
     int probe = 0;  // timing probe IBLB_PROBE_LEVEL (WRONG results): 1 point groups skipped, 2 entry waves skipped,
-                    // 3 point groups end after their region, 4 before their spread, 5 spread
-                    // with plain stores, 6 spread without chunk flags
+                    // 3 point groups end after their region, 4 before their spread (5 / 6, the spread
+                    // with plain stores / without chunk flags: round 5, profiles/r05/probe, removed)
 };
 
 // Two iterations per launch (lbm_sweep.hip): g^t -> g^{t+2}, no IB force owed in between.
