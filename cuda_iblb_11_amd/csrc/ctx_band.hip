@@ -662,9 +662,11 @@ static int band_step(iblb_ctx* c) {
     } else if (c->band_prev_par) {
         // the last cycle's deep sweep (ds) and last level (bs) wrote disjoint parts of g^t; each stream
         // waits for the other's: the chain reads g^t, the deep sweep reads it and overwrites the
-        // buffer the last cycle's chain read (a group slab's ev_bnd follows that deep sweep too: one
-        // barrier packet on the chain's queue instead of two, each ~5 us on the cycle's critical path)
-        if (!(slab && c->bnd_deep)) HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_deep, 0));
+        // buffer the last cycle's chain read.  (ev_bnd is the boundary sweeps' alone: recorded after a
+        // comm-stream wait for the deep sweep as well, it saved the chain one barrier packet but put a
+        // second cross-queue hop between consecutive deep sweeps, ~20 us once the chain had become
+        // shorter than the deep sweep, profiles/r05/combo)
+        HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_deep, 0));
         HIP_TRY(c, hipStreamWaitEvent(ds, c->band_end, 0));
         if (slab) {  // boundary(t-K) wrote columns both read
             HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_bnd, 0));
@@ -678,8 +680,7 @@ static int band_step(iblb_ctx* c) {
         }
     }
     hipStream_t cs = c->comm_stream;
-    // a group slab's boundary sweeps [0, K), [ncol-K, ncol) on the comm stream; ev_bnd follows them and
-    // (PAR) this cycle's deep sweep
+    // a group slab's boundary sweeps [0, K), [ncol-K, ncol) on the comm stream, then ev_bnd
     auto boundary = [&]() -> int {
         Sweep2Args<T> b = sweep_args<T>(c, 0, c->ncol - K, c->ncol, 2, K);  // [0, K) and [ncol-K, ncol)
         b.vs = c->slab_vs;
@@ -700,8 +701,6 @@ static int band_step(iblb_ctx* c) {
             b.wait_err = c->sig_err;
         }
         HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));
-        c->bnd_deep = c->band_par;
-        if (c->bnd_deep) HIP_TRY(c, hipStreamWaitEvent(cs, c->ev_deep, 0));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));
         return IBLB_OK;
     };

@@ -2,8 +2,9 @@
 //
 // Reference: ImmersedBoundary.cu:94-133 (interpolate), :138-267 (spread).  The 3-point delta is
 // zero unless |x-xs| < 1.5 and |y-ys| < 1.5, so a point only touches the 3x3 nodes around
-// (nearbyint(xs), nearbyint(ys)): one 16-lane group per point, one node per lane (lanes 9-15
-// idle), F_s folded across the group in the reference's node order and float rounding, then each
+// (nearbyint(xs), nearbyint(ys)): one nine-lane group per point, one node per lane (seven groups per
+// wave; the merged band launches' groups are 32 lanes, ib_next_group), F_s folded across the group
+// in the reference's node order and float rounding, then each
 // lane spreads its node into a dense force buffer with fp64 atomics (+ a per-(column, chunk) flag
 // the collide-stream kernels read).
 #pragma once
@@ -13,7 +14,7 @@
 namespace iblb {
 
 constexpr int LANES_PER_POINT = 16;
-constexpr int GHOST_PPW = 7;  // ib_ghost_kernel: points per wave (nine lanes each)
+constexpr int GHOST_PPW = 7;  // ib_point_kernel / ib_ghost_kernel: points per wave (nine lanes each)
 
 __device__ __forceinline__ int node_x0(float xs) { return (int)nearbyint((double)xs); }
 
@@ -89,7 +90,7 @@ __device__ __forceinline__ void ib_point_group(const T* __restrict__ g, const La
                                                bool pt, int k, int n, const float* __restrict__ s,
                                                const float* __restrict__ u_s, const int* __restrict__ eps,
                                                float* __restrict__ F_s, double* __restrict__ fd, long fplane,
-                                               uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
+                                               uint8_t* __restrict__ flags, int nch, int rows_per_chunk, int base) {
 #pragma clang fp contract(off)
     float xs = 0.f, ys = 0.f;
     int x = 0, y = 0;
@@ -111,7 +112,7 @@ __device__ __forceinline__ void ib_point_group(const T* __restrict__ g, const La
         }
     }
     float Fx, Fy;
-    fold_terms(tx, ty, valid, Fx, Fy);
+    fold_terms_at(tx, ty, valid, base, Fx, Fy);
     if (!pt || n >= 9) return;
     if (n == 0) {
         F_s[2 * k + 0] = Fx;

@@ -15,8 +15,9 @@
 
 namespace iblb {
 
-// Single slab: one 16-lane group per point does nodes -> F_s -> spread (ib_device.h).  Points are
-// independent (a point's spread needs only its own F_s), so a single-slab step needs one IB launch.
+// Single slab: one nine-lane group per point (seven per wave, lane 63 idle) does nodes -> F_s ->
+// spread (ib_device.h).  Points are independent (a point's spread needs only its own F_s), so a
+// single-slab step needs one IB launch.
 template <typename T>
 __global__ __launch_bounds__(256) void ib_point_kernel(const T* __restrict__ g, Layout L, Halo<T> H, int nx, int ns,
                                                        const float* __restrict__ s, const float* __restrict__ u_s,
@@ -24,9 +25,11 @@ __global__ __launch_bounds__(256) void ib_point_kernel(const T* __restrict__ g, 
                                                        double* __restrict__ fd, long fplane,
                                                        uint8_t* __restrict__ flags, int nch, int rows_per_chunk) {
     const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const int k = (int)(tid / LANES_PER_POINT), n = (int)(tid % LANES_PER_POINT);
+    const int w = (int)(tid >> 6), lane = (int)(tid & 63);
+    const int gp = lane / 9, n = lane - 9 * gp, k = w * GHOST_PPW + gp;
     // no early exit: the whole group takes part in the shuffles
-    ib_point_group<T>(g, L, H, nx, k < ns, k, n, s, u_s, eps, F_s, fd, fplane, flags, nch, rows_per_chunk);
+    ib_point_group<T>(g, L, H, nx, gp < GHOST_PPW && k < ns, k, n, s, u_s, eps, F_s, fd, fplane, flags, nch,
+                      rows_per_chunk, 9 * gp);
 }
 
 template <typename T>
@@ -34,7 +37,7 @@ hipError_t launch_ib_point(const T* g, Layout L, Halo<T> H, int nx, int ns, cons
                            const int* eps, float* F_s, double* fdense, long fplane, uint8_t* flags, int nch,
                            int rows_per_chunk, hipStream_t st) {
     if (ns <= 0) return hipSuccess;
-    const long n = (long)LANES_PER_POINT * ns;
+    const long n = 64L * ((ns + GHOST_PPW - 1) / GHOST_PPW);
     ib_point_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(g, L, H, nx, ns, s, u_s, eps, F_s, fdense, fplane,
                                                                      flags, nch, rows_per_chunk);
     return hipGetLastError();
