@@ -201,6 +201,7 @@ struct iblb_ctx {
     unsigned done_n = 0;          // interior edge waves launched so far (the done word's value once they end)
     unsigned bx_n = 0;            // band cycles whose exchange the level-0 IB signalled in sig[24] (ctx_band.hip)
     bool bx_dev = false;          // this band cycle's boundary sweeps wait on sig[24] (set by band_step)
+    bool bnd_in_end = false;      // the last band cycle's band_end follows its boundary sweeps (ev_bnd)
     bool int_unrec = false;       // the last interior carried no event: ev_int is recorded on demand
     unsigned* sig_err = nullptr;  // host-coherent word: an edge wave's bounded wait timed out
     // profiling

@@ -610,8 +610,15 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
             }
             if (slab && D > 0) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_bnd, 0));
             if (a.ncols <= 0 && a.clr_waves <= 0) HIP_TRY(c, hipEventRecord(c->band_end, ls));
-        } else if (j == K - 1 && a.ncols <= 0 && a.clr_waves <= 0) {  // PAR: right after the chain
-            HIP_TRY(c, hipEventRecord(c->band_end, ls));
+        } else if (j == K - 1) {  // PAR
+            // a group slab's last level after the boundary sweeps too (they are done long before): the
+            // next cycle's streams then wait for band_end alone, one barrier packet per queue fewer
+            // (~5 us each on the critical path once the chain and the deep sweep are equally long)
+            if (slab && bs != ds && (!c->bx_dev || bnd_sub)) {
+                HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_bnd, 0));
+                c->bnd_in_end = true;
+            }
+            if (a.ncols <= 0 && a.clr_waves <= 0) HIP_TRY(c, hipEventRecord(c->band_end, ls));  // right after the chain
         }
         if (a.ncols <= 0 && a.nns <= 0 && a.clr_waves <= 0) continue;
         size_t ev = 0;
@@ -667,8 +674,10 @@ static int band_step(iblb_ctx* c) {
         // second cross-queue hop between consecutive deep sweeps, ~20 us once the chain had become
         // shorter than the deep sweep, profiles/r05/combo)
         HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_deep, 0));
+        // (tried: the deep sweep's waves polling a word a signal kernel sets after the chain, instead of
+        // this barrier: the signal kernel lengthened the chain by ~20 us, profiles/r05/combo4)
         HIP_TRY(c, hipStreamWaitEvent(ds, c->band_end, 0));
-        if (slab) {  // boundary(t-K) wrote columns both read
+        if (slab && !c->bnd_in_end) {  // boundary(t-K) wrote columns both read (bnd_in_end: band_end follows it)
             HIP_TRY(c, hipStreamWaitEvent(bs, c->ev_bnd, 0));
             HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_bnd, 0));
         }
@@ -679,6 +688,7 @@ static int band_step(iblb_ctx* c) {
             HIP_TRY(c, hipStreamWaitEvent(ds, c->ev_bnd, 0));
         }
     }
+    c->bnd_in_end = false;  // (band_chain sets it for this cycle)
     hipStream_t cs = c->comm_stream;
     // a group slab's boundary sweeps [0, K), [ncol-K, ncol) on the comm stream, then ev_bnd
     auto boundary = [&]() -> int {
