@@ -412,7 +412,12 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     // f64: the configured variant (its wall split keeps one wave per SIMD; not with PAR's skip boxes)
     // without the LDS window (bit 7): its 144 KB per workgroup would keep the chain's LDS-using
     // kernels off the deep sweep's CUs (K3 136.0 / 137.1k vs 137.5 / 140.9k MLUPS, profiles/r04/ldswin)
-    d.variant = sizeof(T) == 8 ? c->deep_variant & ~128 : c->band_own_build ? c->deep_variant : c->deep_variant & 1;
+    // f32 group slab (one cell per lane, the chain on CUs of its own): the wall split + preshift, which
+    // takes the skip regions too (round 5, lbm_sweep_impl.h: SPLIT_SKIP)
+    d.variant = sizeof(T) == 8       ? c->deep_variant & ~128
+                : c->band_own_build ? c->deep_variant
+                : slab              ? c->deep_variant & ~(128 | 8)
+                                    : c->deep_variant & 1;
     if (c->band_deep_variant >= 0) d.variant = c->band_deep_variant;  // (A/B: IBLB_BAND_DEEP_VARIANT)
     d.cus = c->ncu ? (slab ? c->ncu - c->reserved_cus : c->ncu) - std::max(0, c->band_reserve) : 0;
     if (c->band_flux >= 0) {

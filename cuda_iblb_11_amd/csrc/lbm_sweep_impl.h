@@ -1096,9 +1096,20 @@ static hipError_t launch_sweepk_vs(const Sweep2Args<T>& a, hipStream_t s, hipEve
         // row (two-cell lanes of the inner chunks never straddle it) holding the last OWN1 or fewer rows
         constexpr int OWN1 = 64 - 2 * ghost_lanes<K, 1>();
         const int top = (a.L.ny - OWN1 + 1) & ~1;
-        if ((a.variant & 2) && (VS == 2 || (a.variant & 64)) && a.nskip == 0 && top > OWN1) {
+        // f32, one cell per lane (a group slab's band cycle): the split with the skip regions too
+        constexpr bool SPLIT_SKIP = sizeof(T) == 4 && VS == 1 && !SLAB;
+        if ((a.variant & 2) && (VS == 2 || (a.variant & 64)) && (a.nskip == 0 || SPLIT_SKIP) && top > OWN1) {
             b.wall_top = top;
             b.wall_ch0 = (top - OWN1 + rows_per_wave - 1) / rows_per_wave;
+            if constexpr (SPLIT_SKIP) {
+                constexpr int WPE = 3;  // (four waves: 6 dwords of scratch spills)
+                if (a.nskip > 0) {
+                    if (a.variant & 32)
+                        return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_PRESHIFT | MODE_SKIP, K, SLAB, WPE>(b, s, stop,
+                                                                                                         start);
+                    return launch_sweepk_mode<T, VS, 1 | MODE_SPLIT | MODE_SKIP, K, SLAB, WPE>(b, s, stop, start);
+                }
+            }
             // bit 3: the inner chunks packed, two waves per SIMD (the packed inner walk needs 191 VGPRs;
             // forced to three waves it spills 21 dwords: 0.417 vs 0.323 ms per M f32 launch, profiles/r04/pack)
             constexpr int WPE = sizeof(T) == 4 ? (VS == 2 ? 3 : 4) : (VS == 2 ? 1 : 2);
