@@ -5,11 +5,11 @@ This package is the host-side mirror of that boundary: `Lattice` (fused context 
 `LocalGroup` / `Lattice.attach_rccl` (x-slab decomposition) and `kernels` (reference-named
 drop-in kernels on device tensors).  There is no CPU fallback.
 """
-from ._lib import IblbError, device_count, load
+from ._lib import IBLB_ERR_ARG, IBLB_ERR_COMM, IBLB_ERR_STATE, IblbError, device_count, load
 from .lattice import (Lattice, LocalGroup, RefParams, plan_slabs, rccl_unique_id, reference_taus,
                       split_populations, split_state)
 
 __all__ = [
-    "IblbError", "device_count", "load", "Lattice", "LocalGroup", "RefParams", "plan_slabs",
+    "IBLB_ERR_ARG", "IBLB_ERR_COMM", "IBLB_ERR_STATE", "IblbError", "device_count", "load", "Lattice", "LocalGroup", "RefParams", "plan_slabs",
     "rccl_unique_id", "reference_taus", "split_populations", "split_state",
 ]

@@ -66,6 +66,7 @@ class Timing(C.Structure):
         ("sweepk_launches", C.c_longlong), ("sweepk_ms", C.c_double), ("sweepk_cells", C.c_longlong), ("sweepk_depth", C.c_longlong),
         ("band_cycles", C.c_longlong), ("band_merged_cycles", C.c_longlong), ("band_par_cycles", C.c_longlong),
         ("deep_launches", C.c_longlong), ("deep_iterations", C.c_longlong),
+        ("dev_wait_launches", C.c_longlong),
     ]
 
 
@@ -118,6 +119,7 @@ _SIGS = {
     "iblb_group_step": ([C.POINTER(_vp), C.c_int, C.c_int], C.c_int),
     "iblb_rccl_unique_id": ([C.c_char_p], C.c_int),
     "iblb_attach_rccl": ([_vp, C.c_char_p, C.c_int, C.c_int], C.c_int),
+    "iblb_set_wait_timeout": ([_vp, C.c_double], C.c_int),
     "iblb_gather_macro": ([_vp, C.c_int, _vp, _vp], C.c_int),
     "iblb_save_checkpoint": ([_vp, C.c_char_p], C.c_int),
     "iblb_load_checkpoint": ([_vp, C.c_char_p], C.c_int),

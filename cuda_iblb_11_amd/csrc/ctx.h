@@ -34,6 +34,7 @@
 #include <climits>
 #include <cstdint>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/iblb.h"
@@ -204,6 +205,19 @@ struct iblb_ctx {
     bool bnd_in_end = false;      // the last band cycle's band_end follows its boundary sweeps (ev_bnd)
     bool int_unrec = false;       // the last interior carried no event: ev_int is recorded on demand
     unsigned* sig_err = nullptr;  // host-coherent word: an edge wave's bounded wait timed out
+    // the device waits' bound (IBLB_WAIT_TIMEOUT_S / iblb_set_wait_timeout, default 600 s): wall-clock
+    // time, in ticks of the device's constant clock (hipDeviceAttributeWallClockRate)
+    double wait_timeout_s = 600.;
+    double clock_hz = 0.;  // the device wall clock's rate
+    unsigned long long wait_ticks = 0;
+    long long dev_wait_launches = 0;  // launches whose waves waited on a device word (iblb_timing)
+    // test hold (IBLB_TEST_HOLD=<n>:<ms>): exchange number n since the attach (0-based) starts after a
+    // one-wave kernel that a host thread releases ms milliseconds after its submission, as if a
+    // neighbour rank reached that exchange late (tests/test_gpu_wait.py)
+    long long hold_x = -1, n_exch = 0;
+    int hold_ms = 0;
+    unsigned* hold_word = nullptr;  // host-coherent
+    std::thread hold_thread;
     // profiling
     int prof = 0;  // 1: events around every launch; 2: the deep launches' own signals only (iblb_set_profiling)
     std::vector<hipEvent_t> ev_pool;
@@ -327,6 +341,8 @@ int ib_ghost(iblb_ctx* c, const void* g, int gc, int clo, int chi, const float* 
              int part, hipStream_t st, unsigned* sig = nullptr, unsigned sig_val = 0, int wlo = 0, int whi = 0);
 int check_ready(iblb_ctx* c);
 int check_wait_err(iblb_ctx* c);  // after a synchronize: did an edge wave's wait time out?
+int set_wait_ticks(iblb_ctx* c);  // wait_ticks from wait_timeout_s and the device's wall-clock rate
+int hold_release(iblb_ctx* c);    // join the test hold's host thread (IBLB_TEST_HOLD)
 int prepare_read(iblb_ctx* c);
 int free_boot(iblb_ctx* c);
 int alloc_zero(iblb_ctx* c, void** p, size_t bytes);

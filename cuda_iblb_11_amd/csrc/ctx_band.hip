@@ -714,6 +714,8 @@ static int band_step(iblb_ctx* c) {
             b.wait_lo = INT_MAX;
             b.wait_hi = INT_MAX;
             b.wait_err = c->sig_err;
+            b.wait_ticks = c->wait_ticks;
+            c->dev_wait_launches++;
         }
         HIP_TRY(c, launch_sweepk<T>(b, K, true, cs));
         HIP_TRY(c, hipEventRecord(c->ev_bnd, cs));

@@ -1,7 +1,10 @@
 // ctx_step.hip — time stepping of a context (ctx.h): the ghost-column halo exchange, the one-step,
 // two-step and deep (K-iteration) schedules of a lone slab and of a slab of a group, iblb_step,
 // local groups, RCCL groups and the output gather.
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "ctx.h"
@@ -35,6 +38,18 @@ int exchange(iblb_ctx* c, hipStream_t st, int d) {
     if (d > c->gc || d > c->ncol) return fail(c, IBLB_ERR_ARG, "halo deeper than the ghost columns or the slab");
     int rc = rccl_order(c, st);
     if (rc) return rc;
+    if (c->hold_x >= 0 && c->n_exch == c->hold_x) {  // IBLB_TEST_HOLD: this exchange starts late
+        if ((rc = hold_release(c))) return rc;
+        __atomic_store_n(c->hold_word, 0u, __ATOMIC_RELEASE);
+        const double bound_s = c->hold_ms * 1e-3 + 60.;
+        HIP_TRY(c, launch_test_hold(c->hold_word, (unsigned long long)(bound_s * c->clock_hz), st));
+        std::fprintf(stderr, "iblb: IBLB_TEST_HOLD: exchange %lld (t = %lld) held for %d ms\n", c->n_exch, c->t, c->hold_ms);
+        c->hold_thread = std::thread([w = c->hold_word, ms = c->hold_ms] {
+            std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+            __atomic_store_n(w, 1u, __ATOMIC_RELEASE);
+        });
+    }
+    ++c->n_exch;
     size_t ev = 0;
     if ((rc = ev_begin(c, &ev, st))) return rc;
     char* g = (char*)c->g[c->cur];
@@ -443,6 +458,8 @@ static int deep_slab_step(iblb_ctx* c, int K) {
                 a.wait_seq = c->sig;
                 a.wait_val = c->sig_n;
                 a.wait_err = c->sig_err;
+                a.wait_ticks = c->wait_ticks;
+                c->dev_wait_launches++;
             }
         }
         size_t ev = 0;
@@ -464,6 +481,8 @@ static int deep_slab_step(iblb_ctx* c, int K) {
             b.wait_lo = INT_MAX;
             b.wait_hi = INT_MAX;
             b.wait_err = c->sig_err;
+            b.wait_ticks = c->wait_ticks;
+            c->dev_wait_launches++;
         }
         HIP_TRY(c, launch_sweepk<T>(b, K, true, bs, stop));
         return IBLB_OK;
@@ -505,15 +524,51 @@ static int deep_slab_step(iblb_ctx* c, int K) {
     return IBLB_OK;
 }
 
-// An edge wave's bounded wait (deep_slab_step) that timed out leaves wrong populations behind: the
-// call that ran it fails (the flag is read after the streams are synchronised).
+// A device wait (deep_slab_step, band_step) that timed out leaves wrong populations behind: the call
+// that ran it fails (the flag is read after the compute stream is synchronised).  With profiling on,
+// the two-way handshake's done word is also checked against the edge-wave count the launcher
+// computed on the host (launch_sweepk_mode's edge_waves): every interior has ended here.
 int check_wait_err(iblb_ctx* c) {
-    if (!c->sig_err || __atomic_load_n(c->sig_err, __ATOMIC_ACQUIRE) == 0) return IBLB_OK;
-    __atomic_store_n(c->sig_err, 0u, __ATOMIC_RELEASE);
-    c->deep_chain = false;
-    return fail(c, IBLB_ERR_COMM,
-                "a slab interior's edge wave timed out waiting for the boundary sweeps of the previous cycle "
-                "(comm stream stalled); the state is invalid");
+    if (!c->sig_err) return IBLB_OK;
+    if (__atomic_load_n(c->sig_err, __ATOMIC_ACQUIRE) != 0) {
+        __atomic_store_n(c->sig_err, 0u, __ATOMIC_RELEASE);
+        c->deep_chain = false;
+        char msg[320];
+        std::snprintf(msg, sizeof msg,
+                      "a device-side wait of the slab hand-off exceeded the wait timeout (%g s, IBLB_WAIT_TIMEOUT_S / "
+                      "iblb_set_wait_timeout): a neighbour rank or the comm stream stalled longer than that; the "
+                      "state is invalid (set it again)",
+                      c->wait_timeout_s);
+        return fail(c, IBLB_ERR_COMM, msg);
+    }
+    if (c->prof == 1 && c->sig && c->done_n) {  // (not in mode 2: the bench's timed regions)
+        unsigned w = 0;
+        HIP_TRY(c, hipMemcpy(&w, c->sig + 16, sizeof w, hipMemcpyDeviceToHost));
+        if (w != c->done_n) {
+            c->deep_chain = false;
+            return fail(c, IBLB_ERR_COMM,
+                        "slab hand-off: the done word (" + std::to_string(w) + ") differs from the edge waves launched (" +
+                            std::to_string(c->done_n) + ")");
+        }
+    }
+    return IBLB_OK;
+}
+
+int set_wait_ticks(iblb_ctx* c) {
+    if (c->clock_hz <= 0.) {
+        int khz = 0;
+        HIP_TRY(c, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+        if (khz <= 0) return fail(c, IBLB_ERR_HIP, "the device reports no wall-clock rate");
+        c->clock_hz = 1e3 * khz;
+    }
+    const double t = c->wait_timeout_s * c->clock_hz;
+    c->wait_ticks = t >= 1.8e19 ? ~0ull : (unsigned long long)t;
+    return IBLB_OK;
+}
+
+int hold_release(iblb_ctx* c) {
+    if (c->hold_thread.joinable()) c->hold_thread.join();
+    return IBLB_OK;
 }
 
 int check_ready(iblb_ctx* c) {
@@ -900,6 +955,21 @@ int iblb_attach_rccl(iblb_ctx* c, const char id[IBLB_UNIQUE_ID_BYTES], int nrank
             c->sig_n = 0;
             c->done_n = 0;
         }
+        if (int rc = set_wait_ticks(c)) return rc;
+        // IBLB_TEST_HOLD=<n>:<ms> (tests): exchange n since this attach starts ms milliseconds late
+        if (const char* h = std::getenv("IBLB_TEST_HOLD")) {
+            long long n = -1;
+            int ms = 0;
+            if (std::sscanf(h, "%lld:%d", &n, &ms) != 2 || n < 0 || ms < 0)
+                return fail(c, IBLB_ERR_ARG, "IBLB_TEST_HOLD: expected <exchange>:<milliseconds>");
+            if (!c->hold_word) {
+                HIP_TRY(c, hipHostMalloc((void**)&c->hold_word, 64, hipHostMallocCoherent));
+                *c->hold_word = 0;
+            }
+            c->hold_x = n;
+            c->hold_ms = ms;
+        }
+        c->n_exch = 0;
         c->bnd_w = INT_MAX;
         c->rccl_last = nullptr;  // the attach's all-gather is complete (synchronised above)
     }

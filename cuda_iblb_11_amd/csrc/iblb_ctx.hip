@@ -267,7 +267,7 @@ static int reset_cilia_state(iblb_ctx* c) {
     return IBLB_OK;
 }
 
-const char* iblb_version(void) { return "iblb-mi355x 0.5 (gfx950, abi 5)"; }
+const char* iblb_version(void) { return "iblb-mi355x 0.6 (gfx950, abi 6)"; }
 int iblb_abi_version(void) { return IBLB_ABI_VERSION; }
 
 int iblb_device_count(int* n) {
@@ -353,7 +353,18 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->deep_balance = (int)env_long("IBLB_DEEP_BALANCE", 1);
     c->band_on = (int)env_long("IBLB_IB_BAND", 1);
     c->band_merge = (int)env_long("IBLB_BAND_MERGE", 1);
+#ifdef IBLB_TIMING_PROBES
+    // timing probes that skip work (WRONG results): only in a build made for them
     c->probe_level = (int)env_long("IBLB_PROBE_LEVEL", 0);
+#else
+    if (env_long("IBLB_PROBE_LEVEL", 0) != 0)
+        std::fprintf(stderr, "iblb: IBLB_PROBE_LEVEL ignored: the library was built without IBLB_TIMING_PROBES\n");
+#endif
+    // the device waits' bound (ctx_step.hip:set_wait_ticks; iblb_set_wait_timeout overrides)
+    if (const char* w = std::getenv("IBLB_WAIT_TIMEOUT_S")) {
+        const double s = std::strtod(w, nullptr);
+        if (s > 0.) c->wait_timeout_s = s;
+    }
     c->band_deep_variant = (int)env_long("IBLB_BAND_DEEP_VARIANT", -1);
     c->wrap_split = (int)env_long("IBLB_WRAP_SPLIT", 1);
     c->band_par_env = (int)env_long("IBLB_BAND_PAR", 1);
@@ -429,6 +440,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
 void iblb_destroy(iblb_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    hold_release(c);  // (a test hold releases its kernel by itself)
     for (hipStream_t s : {c->stream, c->comm_stream})
         if (s) (void)hipStreamSynchronize(s);
     band_release(c);
@@ -444,6 +456,7 @@ void iblb_destroy(iblb_ctx* c) {
         if (p) (void)hipFree(p);
     if (c->sig) (void)hipFree(c->sig);
     if (c->sig_err) (void)hipHostFree(c->sig_err);
+    if (c->hold_word) (void)hipHostFree(c->hold_word);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->left && c->left->right == c) c->left->right = nullptr;
     if (c->right && c->right->left == c) c->right->left = nullptr;
@@ -784,9 +797,11 @@ int iblb_get_timing_ex(iblb_ctx* c, iblb_timing* out, unsigned long bytes, int r
     t->band_par_cycles = c->band_par_cycles;
     t->deep_launches = c->deep_launches;
     t->deep_iterations = c->deep_iterations;
+    t->dev_wait_launches = c->dev_wait_launches;
     if (reset) {
         c->band_cycles = c->band_merged_cycles = c->band_par_cycles = 0;
         c->deep_launches = c->deep_iterations = 0;
+        c->dev_wait_launches = 0;
         c->fused_ms = c->ib_ms = c->halo_ms = c->sweep_ms = c->sweepk_ms = 0.;
         c->fused_launches = c->fused_cells = c->sweep_launches = c->sweep_cells = 0;
         c->sweepk_launches = c->sweepk_cells = 0;
@@ -799,6 +814,14 @@ int iblb_get_stream(iblb_ctx* c, void** stream) {
     if (!c || !stream) return IBLB_ERR_ARG;
     *stream = (void*)c->stream;
     return IBLB_OK;
+}
+
+int iblb_set_wait_timeout(iblb_ctx* c, double seconds) {
+    if (!c || !(seconds > 0.)) return IBLB_ERR_ARG;
+    c->wait_timeout_s = seconds;
+    if (c->clock_hz <= 0.) return IBLB_OK;  // (the ticks are derived at the RCCL attach)
+    HIP_TRY(c, hipSetDevice(c->device));
+    return set_wait_ticks(c);
 }
 
 int iblb_synchronize(iblb_ctx* c) {

@@ -121,13 +121,16 @@ struct Sweep2Args {
     // Device-side ordering of a slab's interior and boundary sweeps (ghost-column builds only,
     // ctx_step.hip:deep_slab_step).  An edge wave is one whose output columns reach below wait_lo or
     // above wait_hi (wait_lo = INT_MAX: every wave).  wait_seq: edge waves first wait until
-    // *wait_seq - wait_val >= 0 (bounded: after ~2 s they set *wait_err and go on; the host reports
-    // it).  done_cnt: edge waves add 1 when their stores are released (agent scope), and the host
-    // learns their number from *edge_waves (set by the launcher).  nullptr: no wait / no signal.
+    // *wait_seq - wait_val >= 0, bounded by wait_ticks of the device's constant wall clock
+    // (wall_clock64; the context's wait timeout, 600 s by default: a neighbour rank that is late
+    // by less never fails the wait); past it they set *wait_err and go on, and the host reports the
+    // call as failed.  done_cnt: edge waves add 1 when their stores are released (agent scope), and
+    // the host learns their number from *edge_waves (set by the launcher).  nullptr: no wait / no signal.
     const unsigned* wait_seq = nullptr;
     unsigned wait_val = 0;
     int wait_lo = 0, wait_hi = 0;
     unsigned* wait_err = nullptr;
+    unsigned long long wait_ticks = 0;
     unsigned* done_cnt = nullptr;
     int* edge_waves = nullptr;  // host pointer, written by launch_sweepk (not read on the device)
     int edge_trim = 0;          // balanced sweeps: the first and last sweep this many columns narrower
@@ -149,6 +152,10 @@ hipError_t launch_sweepk(Sweep2Args<T> a, int depth, bool ghost, hipStream_t s, 
 // *p = v after the stream's previous work (one lane, an agent-scope store: the release of the
 // previous kernel's stores is its end-of-kernel fence)
 hipError_t launch_seq_signal(unsigned* p, unsigned v, hipStream_t s);
+// Test hold (IBLB_TEST_HOLD, ctx_step.hip:exchange): one wave that polls the host-coherent *word
+// until it is non-zero or `ticks` of the device wall clock have passed, so that the work queued
+// behind it on `s` starts late, as behind a neighbour rank that reaches its exchange late.
+hipError_t launch_test_hold(const unsigned* word, unsigned long long ticks, hipStream_t s);
 // Resident waves per CU of a deep-sweep configuration; *nch = its row chunks for ny rows.
 template <typename T>
 int sweepk_geometry(int depth, int vs, int variant, bool ghost, int ny, int* nch);

@@ -67,6 +67,21 @@ hipError_t launch_seq_signal(unsigned* p, unsigned v, hipStream_t s) {
     return hipGetLastError();
 }
 
+// IBLB_TEST_HOLD: the word lives in host-coherent memory (a host thread sets it); one system-scope
+// load per ~8 us, bounded by the wall clock so that the wave always ends
+__global__ __launch_bounds__(64) void test_hold_kernel(const unsigned* word, unsigned long long ticks) {
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+        const unsigned w = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (w != 0 || wall_clock64() - t0 > ticks) break;
+        __builtin_amdgcn_s_sleep(127);
+    }
+}
+hipError_t launch_test_hold(const unsigned* word, unsigned long long ticks, hipStream_t s) {
+    test_hold_kernel<<<1, 64, 0, s>>>(word, ticks);
+    return hipGetLastError();
+}
+
 template hipError_t launch_sweep2<double>(Sweep2Args<double>, bool, hipStream_t);
 template hipError_t launch_sweep2<float>(Sweep2Args<float>, bool, hipStream_t);
 template hipError_t launch_sweepk<double>(Sweep2Args<double>, int, bool, hipStream_t, hipEvent_t, hipEvent_t);

@@ -852,15 +852,19 @@ __device__ __forceinline__ void split_item(const int nin, const int nsw_in, int 
 // signal kernel stores the sequence number (agent scope); here one relaxed agent-scope poll per
 // ~0.2 us (s_sleep), then an agent-scope acquire (this CU's L1) drained by vmcnt(0) before the
 // wave's first load.  Each waiting wave acquires for itself, so no workgroup barrier is needed.
-// Bounded: a signal that never comes (the comm stream failed) must not leave the grid spinning.
-__device__ __forceinline__ void edge_wait(const unsigned* seq, unsigned val, unsigned* err) {
-    constexpr unsigned LIMIT = 1u << 23;  // x ~0.25 us per poll: ~2 s
-    unsigned n = 0;
+// The producer sits behind the cycle's RCCL exchange, i.e. behind the neighbour ranks' hosts: a rank
+// that reaches its next iblb_step late (a file write, a checkpoint, the caller's own work) keeps these
+// waves spinning for as long, as it keeps RCCL's own kernels spinning.  So the bound is wall-clock
+// time, not a poll count: `ticks` of the constant device clock (the context's wait timeout, 600 s by
+// default), only so that a signal that never comes (a failed comm stream or peer) cannot
+// leave the grid spinning for ever; past it the wave flags *err and goes on, and the call fails.
+__device__ __forceinline__ void edge_wait(const unsigned* seq, unsigned val, unsigned* err, unsigned long long ticks) {
+    const unsigned long long t0 = wall_clock64();
     for (;;) {
         const unsigned s = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if ((int)(s - val) >= 0) break;
-        if (++n > LIMIT) {
+        if (wall_clock64() - t0 > ticks) {
             if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             break;
         }
@@ -893,6 +897,7 @@ __host__ __device__ inline void balanced_range(int cb, int ce, int trim, int s, 
     xb = cb - trim + (int)((s + 1) * n / nsw);
     xa = xa < cb ? cb : xa;
     xb = xb > ce ? ce : xb;
+    xb = xb < xa ? xa : xb;  // (the launcher keeps trim below every sweep's share: never empty there)
 }
 
 // G ghost lanes at each wave edge (G * VS >= K - 1 rows)
@@ -928,7 +933,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // an edge wave that signals its stores: write-through in the wall-split walks (the slab builds)
     const bool wt = (MODE & MODE_SPLIT) && edge && a.done_cnt;
     if constexpr (SLAB)
-        if (a.wait_seq && edge) edge_wait(a.wait_seq, a.wait_val, a.wait_err);
+        if (a.wait_seq && edge) edge_wait(a.wait_seq, a.wait_val, a.wait_err, a.wait_ticks);
     const bool rev = sw & 1;
     double q;
     if ((MODE & MODE_SPLIT) && wall) {  // a wall chunk: one cell per lane, the wall walk
@@ -1053,6 +1058,12 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
         waves = (long)b.nsweep * b.wall_ch0 + 2L * b.nsweep_w;
     } else {
         waves = (long)b.nsweep * b.nch;
+    }
+    if (b.col_step <= 0 && b.edge_trim > 0) {
+        // the first and last sweeps keep at least one column: trim < every sweep's share
+        const long n = b.col_end - b.col_begin;
+        const long nsw = std::max((long)b.nsweep, (MODE & MODE_SPLIT) ? (long)b.nsweep_w : 0L);
+        b.edge_trim = (int)std::min((long)b.edge_trim, std::max(0L, n / std::max(1L, nsw) - 1));
     }
     if (b.edge_waves) {  // the waves that will add to done_cnt (sweepk_kernel's `edge`)
         auto edges = [&](int nsw) {

@@ -289,6 +289,11 @@ class Lattice:
         self._check(self._lib.iblb_attach_rccl(self._h, unique_id, int(nranks), int(rank)))
         self.rank = int(rank)
 
+    def set_wait_timeout(self, seconds: float) -> None:
+        """Bound of the group's device-side waits (include/iblb.h iblb_set_wait_timeout; default
+        600 s): a neighbour late by less changes nothing, a longer stall fails the call."""
+        self._check(self._lib.iblb_set_wait_timeout(self._h, float(seconds)))
+
     def gather_macro(self, root: int = 0):
         """Whole-lattice rho [nx*ny], u [2*nx*ny] on rank `root` (None elsewhere); collective."""
         n = self.nx * self.ny

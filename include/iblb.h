@@ -55,8 +55,9 @@ extern "C" {
 
 /* ABI version of this header: bumped whenever a struct crossing the ABI changes layout (iblb_config,
  * iblb_timing, iblb_cilia).  5: iblb_timing's band_cycles ... deep_iterations (round 4), the
- * size-checked iblb_get_timing_ex (round 5).  Compare with iblb_abi_version() at run time. */
-#define IBLB_ABI_VERSION 5
+ * size-checked iblb_get_timing_ex (round 5).  6: iblb_timing's dev_wait_launches, and
+ * iblb_set_wait_timeout (round 6).  Compare with iblb_abi_version() at run time. */
+#define IBLB_ABI_VERSION 6
 
 /* ---------------------------------------------------------------------------------
  * (1) Reference-shaped kernels.  All pointers are DEVICE pointers.  `stream` is a
@@ -163,6 +164,9 @@ typedef struct iblb_timing {
      * no two-iteration or one-step remainder is left where n allows it (ctx_step.hip:deep_depth) */
     long long deep_launches;
     long long deep_iterations;
+    /* launches of an RCCL group slab whose waves waited on a device word instead of a queue wait
+     * (the slab hand-off, iblb_set_wait_timeout below); counted without profiling */
+    long long dev_wait_launches;
 } iblb_timing;
 
 /* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */
@@ -273,6 +277,15 @@ int iblb_link_local(iblb_ctx** ctxs, int n);
 int iblb_group_step(iblb_ctx** ctxs, int n, int nsteps);
 int iblb_rccl_unique_id(char id[IBLB_UNIQUE_ID_BYTES]);
 int iblb_attach_rccl(iblb_ctx* ctx, const char id[IBLB_UNIQUE_ID_BYTES], int nranks, int rank);
+/* Bound of the RCCL group's device-side waits, in seconds of wall-clock time (default 600, or
+ * IBLB_WAIT_TIMEOUT_S from the environment at iblb_create).  Inside a run of deep cycles a slab's
+ * kernels wait for the boundary work of the previous cycle on a device word rather than in the
+ * hardware queue; that work follows the cycle's halo exchange, i.e. the neighbour ranks.  A rank
+ * whose host reaches its next iblb_step late (writing output, a checkpoint, the caller's own work)
+ * delays those waits like RCCL's own kernels and changes no result; only a wait longer than this
+ * bound fails: the iblb_step / iblb_synchronize that sees it returns IBLB_ERR_COMM and the state
+ * must be set again.  Set it at least as long as the longest pause any rank takes between calls. */
+int iblb_set_wait_timeout(iblb_ctx* ctx, double seconds);
 
 /* Whole-lattice rho [nx*ny] and u [2*nx*ny] (reference layout, j = y*XDIM + x) on rank `root`
  * of an RCCL group: the output gather the reference's single-GPU BigData writer needs
