@@ -217,6 +217,27 @@ def pmc_valu(workload_key):
 VALU_PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}
 
 
+_MODE_BITS = ((16, "wall split"), (64, "packed f32x2 collide"), (128, "skip regions"), (256, "preshift"),
+              (512, "LDS window"), (1, "nontemporal stores"))
+
+
+def deep_limiter(tm, valu, precision):
+    """What binds the deep kernel that ran, from the build the library reports for its last deep launch
+    (iblb_timing deep_mode / deep_vs / deep_waves_per_simd / deep_vgprs) and the SQ passes of
+    profiles/pmc_valu.json (VALU issue per wave), not from a fixed string."""
+    mode, vs, wps, vgprs = (int(tm.get(k, 0)) for k in ("deep_mode", "deep_vs", "deep_waves_per_simd", "deep_vgprs"))
+    if wps <= 0:
+        return "dependent latency and VALU issue (DESIGN.md §4)"
+    feats = ", ".join(n for b, n in _MODE_BITS if mode & b) or "plain walk"
+    txt = (f"VALU issue and dependent latency, not HBM: sweepk_kernel<{precision}, {vs} cell(s) per lane, MODE "
+           f"{mode} = {feats}> runs {wps} wave(s) per SIMD at {vgprs} VGPRs")
+    if valu and valu.get("valu_issue_share") is not None:
+        s = float(valu["valu_issue_share"])
+        txt += (f"; each wave issues VALU {100 * s:.0f} % of its cycles, the SIMD ~{100 * min(1.0, s * wps):.0f} % "
+                f"(profiles/pmc_valu.json)")
+    return txt + ". `bound` stays the contract's roofline axis (hbm); the fraction is of HBM peak (DESIGN.md §4)"
+
+
 def pmc_traffic(workload_key):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -491,10 +512,7 @@ def main():
                                   f"HIP events over {min(a.steps, 100)} further steps after the timed region"
                                   + (" (MAX over ranks)" if distributed else "")),
                 "traffic_source": traffic_src,
-                "limiter": (("dependent latency and VALU issue: one wave per SIMD (f64: 256 VGPRs + AGPRs); the K levels of a "
-                             "walk step are a dependent chain (DESIGN.md §4)" if precision == "f64" else
-                             "dependent latency: two waves per SIMD (f32 packed walk, ~200 VGPRs) issue VALU ~37 % of their "
-                             "cycles (DESIGN.md §4)")
+                "limiter": (deep_limiter(tm, valu, precision)
                             if iters_per_launch > 2 else "HBM bandwidth (one read + one write of the state per launch)"),
             },
             # the temporally blocked kernels are bound by vector issue, not HBM: their fp64 / fp32

@@ -67,6 +67,8 @@ class Timing(C.Structure):
         ("band_cycles", C.c_longlong), ("band_merged_cycles", C.c_longlong), ("band_par_cycles", C.c_longlong),
         ("deep_launches", C.c_longlong), ("deep_iterations", C.c_longlong),
         ("dev_wait_launches", C.c_longlong),
+        ("deep_mode", C.c_longlong), ("deep_vs", C.c_longlong), ("deep_waves_per_simd", C.c_longlong),
+        ("deep_vgprs", C.c_longlong),
     ]
 
 

@@ -211,6 +211,7 @@ struct iblb_ctx {
     double clock_hz = 0.;  // the device wall clock's rate
     unsigned long long wait_ticks = 0;
     long long dev_wait_launches = 0;  // launches whose waves waited on a device word (iblb_timing)
+    int deep_kinfo[4] = {0, 0, 0, 0};  // the last deep launch's build: MODE, VS, waves per SIMD, VGPRs (iblb_timing)
     // test hold (IBLB_TEST_HOLD=<n>:<ms>): exchange number n since the attach (0-based) starts after a
     // one-wave kernel that a host thread releases ms milliseconds after its submission, as if a
     // neighbour rank reached that exchange late (tests/test_gpu_wait.py)

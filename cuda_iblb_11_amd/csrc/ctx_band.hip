@@ -432,6 +432,7 @@ static int band_deep(iblb_ctx* c, int K, hipStream_t ds) {
     hipEvent_t e0, e1;  // timing on the launch's own signals (profiling only)
     int rc = ev_kernel(c, &ev, &e0, &e1);
     if (rc) return rc;
+    d.kinfo = c->deep_kinfo;
     HIP_TRY(c, launch_sweepk<T>(d, K, false, ds, e1 ? e1 : (c->band_par ? c->ev_deep : nullptr), e0));
     if (e1 && c->band_par) HIP_TRY(c, hipEventRecord(c->ev_deep, ds));
     c->deep_launches++;

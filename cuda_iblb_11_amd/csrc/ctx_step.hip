@@ -365,6 +365,7 @@ static int sweepk_step(iblb_ctx* c, int d) {
     hipEvent_t e0, e1;  // timing on the launch's own signals (profiling only)
     int rc = ev_kernel(c, &ev, &e0, &e1);
     if (rc) return rc;
+    a.kinfo = c->deep_kinfo;
     HIP_TRY(c, launch_sweepk<T>(a, d, false, c->stream, e1, e0));
     if ((rc = ev_kernel_end(c, ev, EV_SWEEPK, (long long)c->ncol * c->ny))) return rc;
     after_sweep(c, d);
@@ -466,6 +467,7 @@ static int deep_slab_step(iblb_ctx* c, int K) {
         hipEvent_t e0, e1;  // timing on the launch's own signals (profiling only)
         int r = ev_kernel(c, &ev, &e0, &e1);
         if (r) return r;
+        a.kinfo = c->deep_kinfo;
         HIP_TRY(c, launch_sweepk<T>(a, K, hs, c->stream, e1 ? e1 : stop, e0));
         if (e1 && stop) HIP_TRY(c, hipEventRecord(stop, c->stream));
         c->done_n += (unsigned)nedge;

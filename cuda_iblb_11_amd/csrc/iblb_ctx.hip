@@ -798,6 +798,10 @@ int iblb_get_timing_ex(iblb_ctx* c, iblb_timing* out, unsigned long bytes, int r
     t->deep_launches = c->deep_launches;
     t->deep_iterations = c->deep_iterations;
     t->dev_wait_launches = c->dev_wait_launches;
+    t->deep_mode = c->deep_kinfo[0];
+    t->deep_vs = c->deep_kinfo[1];
+    t->deep_waves_per_simd = c->deep_kinfo[2];
+    t->deep_vgprs = c->deep_kinfo[3];
     if (reset) {
         c->band_cycles = c->band_merged_cycles = c->band_par_cycles = 0;
         c->deep_launches = c->deep_iterations = 0;

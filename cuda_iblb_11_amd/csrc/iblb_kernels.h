@@ -133,6 +133,7 @@ struct Sweep2Args {
     unsigned long long wait_ticks = 0;
     unsigned* done_cnt = nullptr;
     int* edge_waves = nullptr;  // host pointer, written by launch_sweepk (not read on the device)
+    int* kinfo = nullptr;       // host pointer: {MODE, VS, resident waves per SIMD, VGPRs} of the build launched
     int edge_trim = 0;          // balanced sweeps: the first and last sweep this many columns narrower
     int nskip = 0;       // > 0: the patch output regions below are left to the band's last level,
     SkipBox skip[MAX_SKIP];  // sorted by x0, disjoint in columns (a lone slab's deep sweep, a group slab's interior and boundary sweeps)

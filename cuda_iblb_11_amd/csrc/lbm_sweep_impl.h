@@ -684,6 +684,18 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
     constexpr int DX = REV ? -1 : 1;
     const int x = x0 + i * DX;
     T N[9][VS];
+    typedef typename VT<T, VS>::type vec;
+    // LDS window, f64: level l+1's moving populations are read from LDS before level l is computed (and
+    // level 2's before level 1), so that the read's latency hides behind a level's arithmetic instead of
+    // stalling the one wave of the SIMD at the start of every level (+12 VGPRs).  The slot read is
+    // written only after its own level's compute, so reading it one level early is the same value.
+    constexpr bool PREF = LW && sizeof(T) == 8;
+    vec pre[lds_npop<T>()];
+    auto lds_slot = [&](int l) { return (vec*)(lw + ((i & 1) * (K - 1) + (l - 2)) * lds_npop<T>() * 64 * VS); };
+    if constexpr (PREF) {
+#pragma unroll
+        for (int p = 0; p < lds_npop<T>(); ++p) pre[p] = lds_slot(2)[p * 64];
+    }
     // fin: the flux column is one of the sweep's outputs; level l reaches it at step fi + l - 1
     level_from_raw<T, VS, MODE>(cur, a, lane, r0, et, walls, fin && i == fi, fown, q, N);
     if (i + 1 < nl1) {
@@ -705,18 +717,22 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
         const bool flux = fin && i == fi + l - 1;
         T out[9][VS];
         const bool made = i >= 2 * (l - 1);
-        typedef typename VT<T, VS>::type vec;
         vec* ls = nullptr;
         if constexpr (LW) {  // slot of parity i: the column made two iterations ago, then this one's
-            ls = (vec*)(lw + ((i & 1) * (K - 1) + (l - 2)) * lds_npop<T>() * 64 * VS);
+            ls = lds_slot(l);
             int p = 0;
 #pragma unroll
             for (int k = 0; k < 9; ++k)
                 if (cx(k) == DX && lds_pop<T>(k)) {
-                    const vec v = ls[p * 64];
+                    const vec v = PREF ? pre[p] : ls[p * 64];
 #pragma unroll
                     for (int e = 0; e < VS; ++e) WA[l - 2][k][e] = v[e];
                     ++p;
+                }
+            if constexpr (PREF)
+                if (l < K) {
+#pragma unroll
+                    for (int p2 = 0; p2 < lds_npop<T>(); ++p2) pre[p2] = lds_slot(l + 1)[p2 * 64];
                 }
         }
         if (made) level_from_window<T, VS, DX, MODE>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, fown, q, out);
@@ -757,7 +773,13 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
             copy_col<T, VS>(WA[l - 2], WB[l - 2]);
             copy_col<T, VS>(WB[l - 2], N);
         }
-        if (l < K && made) copy_col<T, VS>(N, out);
+        // N becomes level l's column for level l+1, made or not: out is left unset when level l is not
+        // made, and level l+1 is then not made either (made(l+1) implies made(l) two iterations back and
+        // now), so whatever N holds there is never used.  Unconditional, the copy is a renaming (the
+        // compiler folds the unset branch away); under `made` it cost 18 v_mov_b64 per level, 108 of
+        // the f64 inner walk step's 144 (round 6).  (f32: the renamed windows need
+        // more registers than three waves per SIMD leave, 168 B of scratch: kept under `made`.)
+        if (l < K && (sizeof(T) == 8 || made)) copy_col<T, VS>(N, out);
     }
 }
 
@@ -765,7 +787,10 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
 // are renamed instead of copied measured 10-20 % slower: more live registers, profiles/r02d_*.)
 // WL: the wave holds a wall row (compile-time, so that the waves of the other chunks carry no
 // wall code and keep no wall planes of the windows live)
-template <typename T, int VS, int MODE, int K, bool SLAB, bool REV, bool WL>
+// NOFLUX: the sweep holds no flux column (the waves of all sweeps but one): the walk is built without
+// the per-level flux test and its branch (round 6: the test's spilled SGPRs cost a v_readlane and a
+// compare per level and cell of every wave)
+template <typename T, int VS, int MODE, int K, bool SLAB, bool REV, bool WL, bool NOFLUX = false>
 __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, int xb, int row0, unsigned off,
                                               int lane, int r0, int et, bool owner, bool bot_, bool top_, T* lw) {
     const bool walls = WL, bot = WL && bot_, top = WL && top_;
@@ -790,7 +815,7 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
     rc[1] = col_rsrc(col_at<T, SLAB>(a, x0));
     rc[2] = col_rsrc(col_at<T, SLAB>(a, x0 + 1));
     load_raw_periodic<T, VS, MODE, SLAB, K>(a, x0, row0, off, bot, top, cur, bo, rc);
-    const bool fin = a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb;
+    const bool fin = !NOFLUX && a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb;
     const int fi = REV ? xb + K - 2 - a.flux_col : a.flux_col - xa + K - 1;  // step of level 1 at the flux column
     // bit e: row r0 + e is owned and its flux sampled; one VGPR computed once (testing the IB
     // band's skipped flux rows inside the walk's flux branch changed the compiled loop: +2 % per
@@ -970,8 +995,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 goto walked;
             }
         }
-        q = rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw)
-                : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw);
+        if (sizeof(T) == 4 || (a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb))  // (f32: spills 20 B)
+            q = rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw)
+                    : sweepk_walk<T, VS, MODE, K, SLAB, false, false>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw);
+        else
+            q = rev ? sweepk_walk<T, VS, MODE, K, SLAB, true, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw)
+                    : sweepk_walk<T, VS, MODE, K, SLAB, false, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, false, false, lw);
     } else {
         const int cs = ch * (OWN * VS);
         const int row0 = cs - G * VS;
@@ -1082,6 +1111,20 @@ static hipError_t launch_sweepk_mode(Sweep2Args<T> b, hipStream_t s, hipEvent_t 
         };
         *b.edge_waves = (MODE & MODE_SPLIT) ? edges(b.nsweep) * b.wall_ch0 + 2 * edges(b.nsweep_w)
                                             : edges(b.nsweep) * b.nch;
+    }
+    if (b.kinfo) {  // which build ran (iblb_timing: the bench line's limiter names it)
+        static int vgprs = -1;
+        if (vgprs < 0) {
+            hipFuncAttributes fa{};
+            vgprs = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&sweepk_kernel<T, VS, MODE, K, SLAB, WPE>)) ==
+                            hipSuccess
+                        ? fa.numRegs
+                        : 0;
+        }
+        b.kinfo[0] = MODE;
+        b.kinfo[1] = VS;
+        b.kinfo[2] = (int)(waves_per_cu<T, VS, MODE, K, SLAB, WPE>() / 4);
+        b.kinfo[3] = vgprs;
     }
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     if (stop || start)  // the events ride on the kernel's own signals: no marker packets around it

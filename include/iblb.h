@@ -55,7 +55,7 @@ extern "C" {
 
 /* ABI version of this header: bumped whenever a struct crossing the ABI changes layout (iblb_config,
  * iblb_timing, iblb_cilia).  5: iblb_timing's band_cycles ... deep_iterations (round 4), the
- * size-checked iblb_get_timing_ex (round 5).  6: iblb_timing's dev_wait_launches, and
+ * size-checked iblb_get_timing_ex (round 5).  6: iblb_timing's dev_wait_launches and deep_mode ... deep_vgprs, and
  * iblb_set_wait_timeout (round 6).  Compare with iblb_abi_version() at run time. */
 #define IBLB_ABI_VERSION 6
 
@@ -167,6 +167,9 @@ typedef struct iblb_timing {
     /* launches of an RCCL group slab whose waves waited on a device word instead of a queue wait
      * (the slab hand-off, iblb_set_wait_timeout below); counted without profiling */
     long long dev_wait_launches;
+    /* the build of the last deep launch (lone slab, slab interior or band cycle's deep sweep): its
+     * MODE bits (lbm_sweep_impl.h), cells per lane, resident waves per SIMD and VGPRs per lane */
+    long long deep_mode, deep_vs, deep_waves_per_simd, deep_vgprs;
 } iblb_timing;
 
 /* Reference defaults: 288x192, TAU/TAU2 for Re=1, T=1e5 (main.cu:267-321). */
