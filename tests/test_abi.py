@@ -124,3 +124,21 @@ def test_abi_version_matches_header():
     assert lib.iblb_abi_version() == v
     assert f"abi {v}" in lib.iblb_version().decode()
     assert lib.iblb_get_timing_ex(None, None, 0, 0) == L.IBLB_ERR_ARG
+
+
+def test_bench_limiter_names_the_build():
+    """bench.py's roofline.limiter is built from the deep build the library reports
+    for its last deep launch (iblb_timing deep_mode / deep_vs / deep_waves_per_simd / deep_vgprs) and the
+    SQ passes' VALU issue share, not from a fixed string."""
+    import importlib.util
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    f32 = bench.deep_limiter({"deep_mode": 593, "deep_vs": 2, "deep_waves_per_simd": 3, "deep_vgprs": 165},
+                             {"valu_issue_share": 0.27}, "f32")
+    assert "3 wave(s) per SIMD at 165 VGPRs" in f32 and "LDS window" in f32 and "packed" in f32, f32
+    assert "27 %" in f32 and "~81 %" in f32 and "(hbm)" in f32, f32
+    f64 = bench.deep_limiter({"deep_mode": 785, "deep_vs": 2, "deep_waves_per_simd": 1, "deep_vgprs": 239}, None, "f64")
+    assert "1 wave(s) per SIMD at 239 VGPRs" in f64 and "preshift" in f64 and "packed" not in f64, f64
+    assert "dependent latency" in bench.deep_limiter({}, None, "f64")

@@ -42,6 +42,7 @@ def test_bench_two_ranks(gpu, workload):
     assert r["frac"] is not None and r["achieved"] > 0 and r["launch_ms"] > 0
     assert r["kernel"].startswith("sweepk_kernel<K=") and "slab interior" in r["kernel"], r["kernel"]
     assert "MAX over ranks" in r["launch_timing"]
+    assert "wave(s) per SIMD at" in r["limiter"] and "MODE" in r["limiter"], r["limiter"]  # the build that ran
     if workload == "K5":
         assert d["ib_band"] is not None and d["ib_band"]["deep_ms_per_cycle"] > 0  # the band cycle ran
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
