@@ -518,7 +518,9 @@ __device__ __forceinline__ void relax_pair(const T (&s)[9][VS], const Sweep2Args
 
 // one column of level l+1 from a window of level l (A = older, B = middle, C = newer column in
 // walking direction DX): the output is B's column; flux: add u_x of the owned rows to q
-template <typename T, int VS, int DX, int MODE = 0>
+// ASH: A's populations that wait in the LDS window arrive already at their pull's rows
+// (lds_pop_read); the others are pulled as usual (LDS window only: no wall rows in those waves)
+template <typename T, int VS, int DX, int MODE = 0, bool ASH = false>
 __device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (&B)[9][VS], const T (&C)[9][VS],
                                                   const Sweep2Args<T>& a, int lane, int r0, int et, bool walls,
                                                   bool flux, int fown, double& q, T (&out)[9][VS]) {
@@ -529,6 +531,13 @@ __device__ __forceinline__ void level_from_window(const T (&A)[9][VS], const T (
     for (int k = 0; k < 9; ++k) pk[k] = cx(k) == DX ? &A[k] : (cx(k) == -DX ? &C[k] : &B[k]);
     T s[9][VS];
     pull_window<T, VS>(pk, nullptr, B[2], B[4], B[7][0], B[8][0], B[5], B[6], lane, r0, et, s, walls);
+    if constexpr (ASH) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+            if (cx(k) == DX && cy(k) != 0)  // (the diagonal movers: in LDS in both precisions)
+#pragma unroll
+                for (int e = 0; e < VS; ++e) s[k][e] = A[k][e];
+    }
     if constexpr (packed_pair<T, VS, MODE>()) {
         relax_pair<T, VS>(s, a, flux, fown, q, out);
         return;
@@ -673,6 +682,20 @@ template <typename T>
 constexpr int lds_npop() { return sizeof(T) == 8 ? 3 : 2; }
 template <typename T, int K, int VS>
 constexpr int lds_window_wave() { return 2 * (K - 1) * lds_npop<T>() * 64 * VS; }  // elements per wave
+// A moving population read back from its LDS slot (q: this lane's vector) at the rows its pull takes
+// (round 6): c_y = +1 reads rows r0-1 .. r0+VS-2, c_y = -1 rows r0+1 .. r0+VS — the neighbour lane's
+// element through the address instead of a DPP row shift after the read (the end lanes read their
+// neighbour block's element or the padding: ghost rows).  c_y = 0: the lane's own vector.
+template <typename T, int VS>
+__device__ __forceinline__ typename VT<T, VS>::type lds_pop_read(const typename VT<T, VS>::type* q, int cyk) {
+    typedef typename VT<T, VS>::type vec;
+    if (cyk == 0) return *q;
+    const T* e0 = (const T*)q - cyk;
+    vec v;
+#pragma unroll
+    for (int e = 0; e < VS; ++e) v[e] = e0[e];
+    return v;
+}
 
 template <typename T, int VS, int MODE, int K, bool SLAB, bool REV, bool LW>
 __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int nl1, int x0, int xa, int xb, int row0,
@@ -692,9 +715,20 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
     constexpr bool PREF = LW && sizeof(T) == 8;
     vec pre[lds_npop<T>()];
     auto lds_slot = [&](int l) { return (vec*)(lw + ((i & 1) * (K - 1) + (l - 2)) * lds_npop<T>() * 64 * VS); };
+    // (the moving populations in LDS, in slot order, and their c_y)
+    auto lds_cy = [](int p) {
+        int q = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+            if (cx(k) == DX && lds_pop<T>(k)) {
+                if (q == p) return cy(k);
+                ++q;
+            }
+        return 0;
+    };
     if constexpr (PREF) {
 #pragma unroll
-        for (int p = 0; p < lds_npop<T>(); ++p) pre[p] = lds_slot(2)[p * 64];
+        for (int p = 0; p < lds_npop<T>(); ++p) pre[p] = lds_pop_read<T, VS>(lds_slot(2) + p * 64, lds_cy(p));
     }
     // fin: the flux column is one of the sweep's outputs; level l reaches it at step fi + l - 1
     level_from_raw<T, VS, MODE>(cur, a, lane, r0, et, walls, fin && i == fi, fown, q, N);
@@ -724,7 +758,7 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
 #pragma unroll
             for (int k = 0; k < 9; ++k)
                 if (cx(k) == DX && lds_pop<T>(k)) {
-                    const vec v = PREF ? pre[p] : ls[p * 64];
+                    const vec v = PREF ? pre[p] : lds_pop_read<T, VS>(ls + p * 64, cy(k));
 #pragma unroll
                     for (int e = 0; e < VS; ++e) WA[l - 2][k][e] = v[e];
                     ++p;
@@ -732,10 +766,10 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
             if constexpr (PREF)
                 if (l < K) {
 #pragma unroll
-                    for (int p2 = 0; p2 < lds_npop<T>(); ++p2) pre[p2] = lds_slot(l + 1)[p2 * 64];
+                    for (int p2 = 0; p2 < lds_npop<T>(); ++p2) pre[p2] = lds_pop_read<T, VS>(lds_slot(l + 1) + p2 * 64, lds_cy(p2));
                 }
         }
-        if (made) level_from_window<T, VS, DX, MODE>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, fown, q, out);
+        if (made) level_from_window<T, VS, DX, MODE, LW>(WA[l - 2], WB[l - 2], N, a, lane, r0, et, walls, flux, fown, q, out);
         // level K's columns of the made steps are exactly the sweep's outputs [xa, xb)
         bool keep = owner;
         if constexpr ((MODE & MODE_SKIP) != 0)
@@ -777,9 +811,12 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
         // made, and level l+1 is then not made either (made(l+1) implies made(l) two iterations back and
         // now), so whatever N holds there is never used.  Unconditional, the copy is a renaming (the
         // compiler folds the unset branch away); under `made` it cost 18 v_mov_b64 per level, 108 of
-        // the f64 inner walk step's 144 (round 6).  (f32: the renamed windows need
-        // more registers than three waves per SIMD leave, 168 B of scratch: kept under `made`.)
-        if (l < K && (sizeof(T) == 8 || made)) copy_col<T, VS>(N, out);
+        // the f64 inner walk step's 144 (round 6).  f64 with the LDS window or one cell
+        // per lane (the wall walks); without the window at two cells per lane (the f64 band cycle's deep
+        // sweep) the renamed windows take 160 instead of 142 AGPRs, which
+        // leaves the band chain's kernels no registers beside the deep sweep's waves (K3 cycle 0.219 ->
+        // 0.277 ms); f32: the renamed windows need more registers than three waves per SIMD leave.
+        if (l < K && ((sizeof(T) == 8 && (LW || VS == 1)) || made)) copy_col<T, VS>(N, out);
     }
 }
 
@@ -934,8 +971,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     T* lw = nullptr;
     if constexpr (lds_window<T, VS, MODE, false>()) {
-        __shared__ __attribute__((aligned(16))) T lwin[4 * lds_window_wave<T, K, VS>()];
-        lw = lwin + wv * lds_window_wave<T, K, VS>() + lane * VS;
+        // (16 B of padding at each end: the shifted reads of lds_pop_read reach one element beyond a
+        // block at the wave's end lanes, whose rows are ghost rows)
+        constexpr int PAD = 16 / (int)sizeof(T);
+        __shared__ __attribute__((aligned(16))) T lwin[4 * lds_window_wave<T, K, VS>() + 2 * PAD];
+        lw = lwin + PAD + wv * lds_window_wave<T, K, VS>() + lane * VS;
     }
     int sw, ch, nsw = a.nsweep;
     bool wall = false;
@@ -977,8 +1017,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 goto walked;
             }
         }
-        q = rev ? sweepk_walk<T, 1, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0, lw)
-                : sweepk_walk<T, 1, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0, lw);
+        // f64: the wall waves are nearly as long as the inner ones, so the flux-free walk here too (f32: the
+        // flux-free one-cell walks measured slower on the K5-width slab, profiles/r06/rings2)
+        if (sizeof(T) == 4 || (a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb))
+            q = rev ? sweepk_walk<T, 1, MODE, K, SLAB, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0, lw)
+                    : sweepk_walk<T, 1, MODE, K, SLAB, false, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0, et == 0, lw);
+        else
+            q = rev ? sweepk_walk<T, 1, MODE, K, SLAB, true, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0,
+                                                                       et == 0, lw)
+                    : sweepk_walk<T, 1, MODE, K, SLAB, false, true, true>(a, xa, xb, row0, off, lane, r0, et, owner, r0 == 0,
+                                                                        et == 0, lw);
     } else if (MODE & MODE_SPLIT) {  // an inner chunk: no wall row within reach of its own rows
         constexpr int OWN1 = 64 - 2 * ghost_lanes<K, 1>();
         const int cs = OWN1 + ch * (OWN * VS);
