@@ -148,6 +148,8 @@ struct iblb_ctx {
     int band_merge = 1;          // IBLB_BAND_MERGE: 1 auto, 2 always, 0 never: each level's launch also
                                  // evaluates the next level's force (merged chain)
     bool band_merged = false;    // the installed plan runs the merged chain
+    int band_vhalf_env = 1;      // IBLB_BAND_VHALF: f32 chained chain's level launches at half-height waves
+    bool band_vhalf = false;     // the installed plan's level entries are in chunks of 64 * V/2 rows
     double* bf_alloc = nullptr;  // merged chain: two more dense force buffers (levels j % 3 = 1, 2) ...
     uint8_t* bfl_alloc = nullptr;  // ... and their chunk flags (zero between cycles)
     double* bfd[2] = {nullptr, nullptr};

@@ -241,7 +241,24 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     // each side (the deep sweep advances every row, the last level overwrites the output rows)
     // (even bounds: a lane of the deep sweep's two-cell walk is then wholly in or out of a patch
     // output, which the deep sweep leaves to the last level when the two run side by side)
-    const int V64 = 64 * c->V;  // rows per chunk of the one-step kernel
+    // the chain's flavour first (the level launches' row chunks depend on it): merged chain (IBLB_BAND_MERGE
+    // 1 = auto) where the chain, not the deep sweep beside it, is the cycle's critical path (the deep sweep
+    // shorter than 1.5x a chain of 2K ~8 us launches: narrow slabs).  Its launches are longer than the
+    // one-step launches they replace (the point groups recompute the level's collide over their nodes'
+    // pulls): beside a long deep sweep it only adds work (K3 0.0378 vs 0.0359 ms/iteration); on the
+    // K5-width slab it saves 3-6 % (profiles/r03mg)
+    const long long deep_cols = slab ? std::max(0, ncol - 2 * K) : ncol;  // the deep sweep's columns
+    {
+        const double deep_us = (double)K * deep_cols * ny / (is_f64(c) ? 130e3 : 190e3);
+        c->band_merged = c->band_merge == 2 || (c->band_merge == 1 && deep_us < 1.5 * 2 * K * 8.0);
+    }
+    // Half-height level waves (f32 chained chain, IBLB_BAND_VHALF, round 6): a level launch's waves take
+    // 64 * V/2 rows (two cells per lane) instead of 64 * V: a patch's row range (K5's filaments: ~110
+    // rows) then spans fewer padding rows than in 256-row chunks, and the chain — K5's critical path
+    // beside the deep sweep (profiles/r06/k5tl) — computes fewer cells
+    c->band_vhalf = !is_f64(c) && !c->band_merged && c->band_vhalf_env != 0;
+    const int V64 = 64 * (c->band_vhalf ? c->V / 2 : c->V);  // rows per chunk of the level launches
+    const int nchv = (ny + V64 - 1) / V64;                     // such chunks per column
     std::vector<std::array<int, 2>> pr(b.size());
     for (size_t q = 0; q < b.size(); ++q)
         pr[q] = {std::max(0, b[q][2] - (K - 1)) & ~1, std::min(ny, (b[q][3] + K + 1) & ~1)};
@@ -255,7 +272,7 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
         const int lj = -bd + 1 + j, hj = ncol + bd - 2 - j;  // columns level j can compute
         for (size_t q = 0; q < b.size(); ++q) {
             const int ylo = std::max(0, pr[q][0] - m), yhi = std::min(ny, pr[q][1] + m);
-            const int ch0 = ylo / V64, ch1 = std::min(c->nch, (yhi + V64 - 1) / V64);
+            const int ch0 = ylo / V64, ch1 = std::min(nchv, (yhi + V64 - 1) / V64);
             int xa = std::max(b[q][0] - R + j, lj), xb = std::min(b[q][1] + R - j, hj);
             if (j == K - 1) {  // the last level stores the slab's own columns only
                 xa = std::max(xa, 0);
@@ -271,13 +288,14 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
         }
     }
     if (!slab && 2 * band_lu > (long long)K * nx * ny) return IBLB_OK;
-    // the deep sweep: every column of a lone slab, the interior [K, ncol-K) of a group slab
-    const long long deep_cols = slab ? std::max(0, ncol - 2 * K) : ncol;
+    // the deep sweep: every column of a lone slab, the interior [K, ncol-K) of a group slab (deep_cols)
     int rc = band_streams(c, band_lu / std::max(1, ny), deep_cols);
     if (rc) return rc;
     // the tables go to a ring of pinned (device-visible, coherent) host slots that the cycle's
     // launches read directly: a new plan of moving points costs no copy on the cycle's critical
-    // path; a slot is rewritten only after the event of the last cycle that read it
+    // path; a slot is rewritten only after the event of the last cycle that read it.  (Round 6 tried a
+    // device copy of each new plan's slot on the chain's stream: K5, whose moving points bring a new plan
+    // every cycle, 0.52-0.62 ms per cycle against 0.441-0.445; K3's static plan equal, profiles/r06/dt1)
     if (tab.size() > c->band_pin_cap) {  // every slot may be in use: wait for the cycles in flight
         if ((rc = band_join(c))) return rc;
         HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -298,15 +316,6 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
     if (!tab.empty()) std::memcpy(c->band_pin[slot], tab.data(), tab.size() * sizeof(int));
     c->band_tab = c->band_pin[slot];
     c->band_pin_cur = slot;
-    // merged chain (IBLB_BAND_MERGE 1 = auto): where the chain, not the deep sweep beside it, is the
-    // cycle's critical path (the deep sweep shorter than 1.5x a chain of 2K ~8 us launches: narrow
-    // slabs).  Its launches are longer than the one-step launches they replace (the point groups
-    // recompute the level's collide over their nodes' pulls): beside a long deep sweep it only adds
-    // work (K3 0.0378 vs 0.0359 ms/iteration); on the K5-width slab it saves 3-6 % (profiles/r03mg)
-    {
-        const double deep_us = (double)K * deep_cols * ny / (is_f64(c) ? 130e3 : 190e3);
-        c->band_merged = c->band_merge == 2 || (c->band_merge == 1 && deep_us < 1.5 * 2 * K * 8.0);
-    }
     if (c->band_merged && !c->bf_alloc) {  // merged chain: the force buffers of levels j % 3 = 1, 2
         const size_t width = (size_t)c->ncol + 2 * c->gc;
         if ((rc = alloc_zero(c, (void**)&c->bf_alloc, 4 * (size_t)c->fplane * sizeof(double)))) return rc;
@@ -550,6 +559,7 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
         a.row_tab = 1;
         a.nchl = c->band_nchl[j];
         a.store_rows = j == K - 1;  // the last level writes g^{t+K}: patch output rows only
+        a.vhalf = !merged && c->band_vhalf;  // the plan's chunks are 64 * V/2 rows then
         a.flags = merged ? fl[j % 3] : c->flags;
         a.fdense = merged ? fd[j % 3] : c->fdense;
         a.fplane = c->fplane;
@@ -630,7 +640,7 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
         size_t ev = 0;
         if ((rc = ev_begin(c, &ev, ls))) return rc;
         HIP_TRY(c, launch_fused<T>(a, ls, j == K - 1 ? c->band_end : nullptr));
-        if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * a.nchl * 64 * c->V, ls))) return rc;
+        if ((rc = ev_end(c, ev, EV_FUSED, (long long)a.ncols * a.nchl * 64 * (a.vhalf ? c->V / 2 : c->V), ls))) return rc;
         // bx_dev: the boundary sweeps after their producer (the level-0 IB) and after the first level,
         // so that their host-side submission does not delay the chain's first launches
         if (j == 0 && c->bx_dev && !bnd_sub) {

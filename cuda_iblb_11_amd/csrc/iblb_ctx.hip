@@ -368,6 +368,7 @@ int iblb_create(const iblb_config* cfg, iblb_ctx** out) {
     c->band_deep_variant = (int)env_long("IBLB_BAND_DEEP_VARIANT", -1);
     c->wrap_split = (int)env_long("IBLB_WRAP_SPLIT", 1);
     c->band_par_env = (int)env_long("IBLB_BAND_PAR", 1);
+    c->band_vhalf_env = (int)env_long("IBLB_BAND_VHALF", 1);
     // cells per lane in a group slab's deep sweeps: f64 two (the wall split needs them: self ring
     // 512 / 1024 / 2048 x 4096 0.0170 / 0.0293 / 0.0531 ms/iteration vs 0.0194 / 0.0343 / 0.0638
     // with one, profiles/r04/split64); f32 one (1024 / 2048 x 2048: 0.0126 / 0.0203 vs 0.0133 /

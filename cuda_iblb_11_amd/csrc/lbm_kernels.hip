@@ -96,9 +96,11 @@ __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, 
             if (e == et) { v4[e] = t2; v8[e] = t5; v7[e] = t6; }
     }
 
-    // dense IB force for this (column, chunk), consumed and cleared
+    // dense IB force for this (column, chunk), consumed and cleared (vhalf: the flag of the 64*2V-row
+    // chunk this half-height wave lies in, left set: the other half-height wave may not have read it)
+    const long fi = (long)xc * a.nch + (a.vhalf ? ch >> 1 : ch);
     bool has_f = false;
-    if (IB) has_f = a.flags[((long)xc * a.nch + ch)] != 0;
+    if (IB) has_f = a.flags[fi] != 0;
     double fxv[V], fyv[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) { fxv[e] = 0.; fyv[e] = 0.; }
@@ -110,7 +112,7 @@ __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, 
         if (!a.fkeep) {
 #pragma unroll
             for (int e = 0; e < V; ++e) { fx[e] = 0.; fy[e] = 0.; }
-            if (lane == 0) a.flags[(long)xc * a.nch + ch] = 0;  // only this wave reads this flag
+            if (lane == 0 && !a.vhalf) a.flags[fi] = 0;  // only this wave reads this flag
         }
     }
     if (IB && a.flclr) band_clear<V>(a.fdclr, a.flclr, a.fplane, L.rows, a.nch, xc, ch, y0, lane);
@@ -210,6 +212,15 @@ template <typename T, int MODE>
 hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t s, hipEvent_t stop) {
     constexpr int V = vec_of<T>();
     if (a.row_tab && (a.nns > 0 || a.clr_waves > 0)) return launch_band_level_mode<T, MODE>(a, blocks, s, stop);
+    if constexpr (sizeof(T) == 4)
+        if (a.vhalf) {  // band levels in half-height waves (f32: two cells per lane, 128-row chunks)
+            if (!a.row_tab || a.fkeep || a.flclr) return hipErrorInvalidValue;
+            if (stop)
+                hipExtLaunchKernelGGL(fused_kernel<T, V / 2, true, MODE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, a);
+            else
+                fused_kernel<T, V / 2, true, MODE><<<blocks, 256, 0, s>>>(a);
+            return hipGetLastError();
+        }
     if (stop) {  // the event rides on the kernel's own completion signal: no marker packet after it
         if (a.flags)
             hipExtLaunchKernelGGL(fused_kernel<T, V, true, MODE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, a);

@@ -859,6 +859,31 @@ def test_ib_band_merged_equals_chained(gpu, oracle, precision, monkeypatch):
     assert abs(runs["2"][2] - runs["0"][2]) <= (1e-11 if precision == "f64" else 1e-5) * max(abs(runs["0"][2]), 1e-30)
 
 
+def test_ib_band_half_height_levels(gpu, oracle, monkeypatch):
+    """f32 chained chain with half-height level waves (IBLB_BAND_VHALF=1, the default: 128-row chunks,
+    the IB flags still per 256 rows, read by both halves and left set) against full-height ones (=0),
+    on 600 rows with filaments across the 128- and 256-row chunk bounds and near the top wall: equal
+    up to the arrival order of the spread atomics, both against the oracle, and fewer fused-launch cells."""
+    nx, ny = 160, 600
+    a, b, c = _line(40.3, 70, y0=100.0), _line(90.7, 60, y0=230.0), _line(130.2, 40, y0=555.0)
+    pts = tuple(np.concatenate([p, q, r]) for p, q, r in zip(a, b, c))
+    monkeypatch.setenv("IBLB_BAND_MERGE", "0")
+    runs = {}
+    for vh in ("1", "0"):
+        monkeypatch.setenv("IBLB_BAND_VHALF", vh)
+        lat, sim = _static_run(gpu, oracle, nx, ny, 4 * K + 3, pts, chunks=(2, 2 * K, K + 1, K), precision="f32",
+                               monkeypatch=monkeypatch)
+        tm = lat.timing()
+        assert tm["sweepk_launches"] >= 3, tm
+        runs[vh] = (lat.macro(), lat.force(), lat.flux, tm)
+        check_fields(lat, sim, TOL32)
+        lat.close()
+    assert runs["1"][3]["fused_cells"] < runs["0"][3]["fused_cells"], (runs["1"][3], runs["0"][3])
+    (r1, u1), (r0, u0) = runs["1"][0], runs["0"][0]
+    assert rel(r1, r0) <= 1e-6 and rel(u1, u0) <= 1e-5
+    assert abs(runs["1"][2] - runs["0"][2]) <= 1e-5 * max(abs(runs["0"][2]), 1e-30)
+
+
 def _ulps(a, b):
     """Distance of two float32 arrays in units in the last place."""
     ia = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
