@@ -39,6 +39,9 @@ namespace iblb {
 
 // sweep only (MODE bits 1, 2 as in lbm_vec.h): no software prefetch of the next column (two-step
 // sweeps); the deep sweep's wall split (sweepk_kernel)
+#ifndef IBLB_WALK_UL
+#define IBLB_WALK_UL 1  // the LDS-window walks load the next column unconditionally (0: round 6's A/B base)
+#endif
 enum { MODE_NO_PREFETCH = 8, MODE_SPLIT = 16, MODE_PACK = 64, MODE_SKIP = 128, MODE_PRESHIFT = 256, MODE_LDSWIN = 512,
        MODE_WT_STORE = 1024 };
 
@@ -697,7 +700,10 @@ __device__ __forceinline__ typename VT<T, VS>::type lds_pop_read(const typename 
     return v;
 }
 
-template <typename T, int VS, int MODE, int K, bool SLAB, bool REV, bool LW>
+// UL (the LDS-window walks, round 6): the next column's loads are unconditional, the last step loading
+// columns it already read (x - DX .. x + DX: inside the walk's reach): the loaded column then needs no
+// select against the old one at the loop's back edge (18 v_mov_b64 per f64 step)
+template <typename T, int VS, int MODE, int K, bool SLAB, bool REV, bool LW, bool UL = false>
 __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int nl1, int x0, int xa, int xb, int row0,
                                             unsigned off, int lane, int r0, int et, bool owner, bool bot, bool top,
                                             bool walls, T (&WA)[K - 1][9][VS], T (&WB)[K - 1][9][VS],
@@ -732,18 +738,19 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
     }
     // fin: the flux column is one of the sweep's outputs; level l reaches it at step fi + l - 1
     level_from_raw<T, VS, MODE>(cur, a, lane, r0, et, walls, fin && i == fi, fown, q, N);
-    if (i + 1 < nl1) {
+    if (UL || i + 1 < nl1) {
         // the resources of the next column triple: one new column
+        const int xl = UL && i + 1 >= nl1 ? x - DX : x;
         if (DX > 0) {
             rc[0] = rc[1];
             rc[1] = rc[2];
-            rc[2] = col_rsrc(col_at<T, SLAB>(a, x + 2));
+            rc[2] = col_rsrc(col_at<T, SLAB>(a, xl + 2));
         } else {
             rc[2] = rc[1];
             rc[1] = rc[0];
-            rc[0] = col_rsrc(col_at<T, SLAB>(a, x - 2));
+            rc[0] = col_rsrc(col_at<T, SLAB>(a, xl - 2));
         }
-        load_raw_periodic<T, VS, MODE, SLAB, K>(a, x + DX, row0, off, bot, top, cur, bo, rc);
+        load_raw_periodic<T, VS, MODE, SLAB, K>(a, xl + DX, row0, off, bot, top, cur, bo, rc);
     }
 #pragma unroll
     for (int l = 2; l <= K; ++l) {
@@ -871,10 +878,13 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
             }
         skip_load<T, VS, REV>(a, r0, sp);
     }
+    // (round 6 also tried two steps per trip with WA and WB swapping roles, the window's rotation a
+    // renaming: the compiler kept the windows in AGPRs, 1399 instructions per f64 step against 1392)
+    constexpr bool LW = lds_window<T, VS, MODE, WL>();
     for (int i = 0; i < nl1; ++i)
-        sweepk_iter<T, VS, MODE, K, SLAB, REV, lds_window<T, VS, MODE, WL>()>(a, i, nl1, x0, xa, xb, row0, off, lane, r0, et,
-                                                                        owner, bot, top, walls, WA, WB, cur, q, bo, rc,
-                                                                        fin, fi, fown, sp, lw);
+        sweepk_iter<T, VS, MODE, K, SLAB, REV, LW, LW && IBLB_WALK_UL>(a, i, nl1, x0, xa, xb, row0, off, lane, r0, et, owner,
+                                                                    bot, top, walls, WA, WB, cur, q, bo, rc, fin, fi, fown,
+                                                                    sp, lw);
     return q;
 }
 
