@@ -426,6 +426,31 @@ template <typename T, bool SLAB>
 __device__ __forceinline__ const T* col_at(const Sweep2Args<T>& a, int x) {
     return SLAB ? a.src + (long)x * a.L.col : col_wrap(a, x);
 }
+// The walk's column pointers kept from step to step (UL walks, round 6): the next column to load (pn,
+// its periodic index xn in a lone slab) and the output column (pd) advance by one column stride
+// instead of a periodic wrap and a 64-bit multiply per step (~30 scalar instructions, an issue slot
+// each at one wave per SIMD)
+template <typename T>
+struct ColPtrs {
+    const T* pn;
+    int xn;
+    T* pd;
+};
+template <typename T, bool SLAB, int DX>
+__device__ __forceinline__ void col_step(const Sweep2Args<T>& a, const T*& p, int& xw) {
+    p += DX * (long)a.L.col;
+    if (!SLAB) {
+        xw += DX;
+        if (DX > 0 && xw == a.L.ncol) {
+            xw = 0;
+            p = a.src;
+        }
+        if (DX < 0 && xw < 0) {
+            xw = a.L.ncol - 1;
+            p = a.src + (long)(a.L.ncol - 1) * a.L.col;
+        }
+    }
+}
 template <typename T, int VS, int MODE>
 __device__ __forceinline__ void ld_rows_buf(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff, T v[VS]) {
     typedef typename VT<T, VS>::type vec;
@@ -709,9 +734,10 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
                                             bool walls, T (&WA)[K - 1][9][VS], T (&WB)[K - 1][9][VS],
                                             Raw<T, VS>& cur, double& q, const BufOfs& bo,
                                             __amdgpu_buffer_rsrc_t (&rc)[3], bool fin, int fi, int fown, SkipState& sp,
-                                            T* lw) {
+                                            T* lw, ColPtrs<T>& cp) {
     constexpr int DX = REV ? -1 : 1;
     const int x = x0 + i * DX;
+    if constexpr (UL) cp.pd += DX * (long)a.L.col;  // output column x - (K-1) DX
     T N[9][VS];
     typedef typename VT<T, VS>::type vec;
     // LDS window, f64: level l+1's moving populations are read from LDS before level l is computed (and
@@ -741,14 +767,21 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
     if (UL || i + 1 < nl1) {
         // the resources of the next column triple: one new column
         const int xl = UL && i + 1 >= nl1 ? x - DX : x;
+        __amdgpu_buffer_rsrc_t rn;
+        if constexpr (UL) {  // column xl + 2 DX: the last step keeps the previous one (x + DX)
+            if (i + 1 < nl1) col_step<T, SLAB, DX>(a, cp.pn, cp.xn);
+            rn = col_rsrc(cp.pn);
+        } else {
+            rn = col_rsrc(col_at<T, SLAB>(a, xl + 2 * DX));
+        }
         if (DX > 0) {
             rc[0] = rc[1];
             rc[1] = rc[2];
-            rc[2] = col_rsrc(col_at<T, SLAB>(a, xl + 2));
+            rc[2] = rn;
         } else {
             rc[2] = rc[1];
             rc[1] = rc[0];
-            rc[0] = col_rsrc(col_at<T, SLAB>(a, xl - 2));
+            rc[0] = rn;
         }
         load_raw_periodic<T, VS, MODE, SLAB, K>(a, xl + DX, row0, off, bot, top, cur, bo, rc);
     }
@@ -782,7 +815,7 @@ __device__ __forceinline__ void sweepk_iter(const Sweep2Args<T>& a, int i, int n
         if constexpr ((MODE & MODE_SKIP) != 0)
             if (made && l == K) keep = owner && !skip_rows<T, VS, REV>(a, c, r0, sp);
         if (made && l == K && keep) {
-            const __amdgpu_buffer_rsrc_t rd = col_rsrc<T>(a.dst + (long)c * a.L.col);
+            const __amdgpu_buffer_rsrc_t rd = col_rsrc<T>(UL ? cp.pd : a.dst + (long)c * a.L.col);
 #pragma unroll
             for (int k = 0; k < 9; ++k) st_rows_buf<T, VS, MODE>(rd, bo.lane, (unsigned)k * bo.plane, out[k]);
         }
@@ -858,6 +891,15 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
     rc[0] = col_rsrc(col_at<T, SLAB>(a, x0 - 1));
     rc[1] = col_rsrc(col_at<T, SLAB>(a, x0));
     rc[2] = col_rsrc(col_at<T, SLAB>(a, x0 + 1));
+    constexpr int DX = REV ? -1 : 1;
+    ColPtrs<T> cp;
+    cp.pn = col_at<T, SLAB>(a, x0 + DX);
+    {
+        const int n = a.L.ncol;
+        int xw = (x0 + DX) % n;
+        cp.xn = xw < 0 ? xw + n : xw;
+    }
+    cp.pd = a.dst + (long)(x0 - K * DX) * a.L.col;  // (advanced before its first use: column x0 - (K-1) DX)
     load_raw_periodic<T, VS, MODE, SLAB, K>(a, x0, row0, off, bot, top, cur, bo, rc);
     const bool fin = !NOFLUX && a.flux_col >= 0 && a.flux_col >= xa && a.flux_col < xb;
     const int fi = REV ? xb + K - 2 - a.flux_col : a.flux_col - xa + K - 1;  // step of level 1 at the flux column
@@ -884,7 +926,7 @@ __device__ __forceinline__ double sweepk_walk(const Sweep2Args<T>& a, int xa, in
     for (int i = 0; i < nl1; ++i)
         sweepk_iter<T, VS, MODE, K, SLAB, REV, LW, LW && IBLB_WALK_UL>(a, i, nl1, x0, xa, xb, row0, off, lane, r0, et, owner,
                                                                     bot, top, walls, WA, WB, cur, q, bo, rc, fin, fi, fown,
-                                                                    sp, lw);
+                                                                    sp, lw, cp);
     return q;
 }
 
