@@ -252,11 +252,11 @@ static int plan_bands_t(iblb_ctx* c, const std::vector<float>& xy) {
         const double deep_us = (double)K * deep_cols * ny / (is_f64(c) ? 130e3 : 190e3);
         c->band_merged = c->band_merge == 2 || (c->band_merge == 1 && deep_us < 1.5 * 2 * K * 8.0);
     }
-    // Half-height level waves (f32 chained chain, IBLB_BAND_VHALF, round 6): a level launch's waves take
+    // Half-height level waves (f32, IBLB_BAND_VHALF, round 6): a level launch's entry waves take
     // 64 * V/2 rows (two cells per lane) instead of 64 * V: a patch's row range (K5's filaments: ~110
     // rows) then spans fewer padding rows than in 256-row chunks, and the chain — K5's critical path
     // beside the deep sweep (profiles/r06/k5tl) — computes fewer cells
-    c->band_vhalf = !is_f64(c) && !c->band_merged && c->band_vhalf_env != 0;
+    c->band_vhalf = !is_f64(c) && c->band_vhalf_env != 0;
     const int V64 = 64 * (c->band_vhalf ? c->V / 2 : c->V);  // rows per chunk of the level launches
     const int nchv = (ny + V64 - 1) / V64;                     // such chunks per column
     std::vector<std::array<int, 2>> pr(b.size());
@@ -559,7 +559,7 @@ static int band_chain(iblb_ctx* c, int K, const T* A, T* B, T* const S[2], bool 
         a.row_tab = 1;
         a.nchl = c->band_nchl[j];
         a.store_rows = j == K - 1;  // the last level writes g^{t+K}: patch output rows only
-        a.vhalf = !merged && c->band_vhalf;  // the plan's chunks are 64 * V/2 rows then
+        a.vhalf = c->band_vhalf;  // the plan's chunks are 64 * V/2 rows then
         a.flags = merged ? fl[j % 3] : c->flags;
         a.fdense = merged ? fd[j % 3] : c->fdense;
         a.fplane = c->fplane;

@@ -80,10 +80,10 @@ struct FusedArgs {
     // the nns point groups, whose groups then take image m = 0 only (a point at the lattice's x edge
     // has two images in a slab touching that edge, which one group would walk one after the other)
     int wlo = 0, whi = 0;
-    // vhalf (band cycle, chained chain): the launch runs 64 * V/2-row waves (row_tab chunks in those
+    // vhalf (band cycle, f32): the launch's entry waves take 64 * V/2 rows (row_tab chunks in those
     // units); the IB flags stay per 64 * V rows, read at chunk / 2 and not cleared by these waves (two
     // waves share one: a flag left set over zeroed force takes the forced collide with force 0, bit
-    // for bit the unforced one)
+    // for bit the unforced one; a merged level's fdclr values are still cleared, their flag kept)
     int vhalf = 0;
     int probe = 0;  // timing probe IBLB_PROBE_LEVEL (WRONG results): 1 point groups skipped, 2 entry waves skipped,
                     // 3 point groups end after their region, 4 before their spread (5 / 6, the spread

@@ -14,15 +14,16 @@
 namespace iblb {
 
 // merged band chain: clear the force buffer the previous launch consumed at (column xc, chunk ch)
+// (the lane's rows y0 .. y0+V-1; clear_flag false: half-height waves, two of them per flag, leave it set)
 template <int V>
 __device__ __forceinline__ void band_clear(double* fd, uint8_t* fl, long fplane, int rows, int nch, int xc, int ch,
-                                           int y0, int lane) {
+                                           int y0, int lane, bool clear_flag = true) {
     const long fi = (long)xc * nch + ch;
     if (fl[fi]) {
         double* p = fd + (long)xc * rows + y0;
 #pragma unroll
         for (int e = 0; e < V; ++e) { p[e] = 0.; p[fplane + e] = 0.; }
-        if (lane == 0) fl[fi] = 0;
+        if (lane == 0 && clear_flag) fl[fi] = 0;
     }
 }
 
@@ -115,7 +116,7 @@ __device__ __forceinline__ void fused_wave(const FusedArgs<T>& a, const int gw, 
             if (lane == 0 && !a.vhalf) a.flags[fi] = 0;  // only this wave reads this flag
         }
     }
-    if (IB && a.flclr) band_clear<V>(a.fdclr, a.flclr, a.fplane, L.rows, a.nch, xc, ch, y0, lane);
+    if (IB && a.flclr) band_clear<V>(a.fdclr, a.flclr, a.fplane, L.rows, a.nch, xc, a.vhalf ? ch >> 1 : ch, y0, lane, !a.vhalf);
 
     const bool do_flux = a.flux_col >= 0 && xc == a.flux_col;  // (-1: none; ghost column -1 is a real column)
     double q = 0.;
@@ -166,7 +167,8 @@ __global__ __launch_bounds__(256) void fused_kernel(FusedArgs<T> a) {
 // groups of the next level's IB (ib_next_group) first — the launch's longest waves, dispatched before
 // the others — then the waves of the table entries (fused_wave), then clr_waves clear-only waves.  The
 // roles are wave-uniform; the point groups synchronise only within their wave (LDS region per group).
-template <typename T, int V, int MODE>
+// (VW: cells per lane of the entry waves, V/2 with FusedArgs::vhalf; the IB flags stay per 64*V rows)
+template <typename T, int V, int MODE, int VW = V>
 __global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
     __shared__ T reg[256 / NEXT_LANES][NEXT_CELLS][9];
     const int lane = threadIdx.x & 63;
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
     }
     const int w = gw - pw, ew = a.ncols * a.nchl;
     if (w < ew) {
-        if (a.probe != 2) fused_wave<T, V, true, MODE>(a, w, lane);
+        if (a.probe != 2) fused_wave<T, VW, true, MODE>(a, w, lane);
         return;
     }
     if (w < ew + a.clr_waves) {
@@ -201,6 +203,15 @@ __global__ __launch_bounds__(256) void band_level_kernel(FusedArgs<T> a) {
 template <typename T, int MODE>
 hipError_t launch_band_level_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t s, hipEvent_t stop) {
     constexpr int V = vec_of<T>();
+    if constexpr (sizeof(T) == 4)
+        if (a.vhalf) {
+            if (stop)
+                hipExtLaunchKernelGGL(band_level_kernel<T, V, MODE, V / 2>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0,
+                                      a);
+            else
+                band_level_kernel<T, V, MODE, V / 2><<<blocks, 256, 0, s>>>(a);
+            return hipGetLastError();
+        }
     if (stop)
         hipExtLaunchKernelGGL(band_level_kernel<T, V, MODE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, a);
     else
@@ -214,7 +225,7 @@ hipError_t launch_fused_mode(const FusedArgs<T>& a, unsigned blocks, hipStream_t
     if (a.row_tab && (a.nns > 0 || a.clr_waves > 0)) return launch_band_level_mode<T, MODE>(a, blocks, s, stop);
     if constexpr (sizeof(T) == 4)
         if (a.vhalf) {  // band levels in half-height waves (f32: two cells per lane, 128-row chunks)
-            if (!a.row_tab || a.fkeep || a.flclr) return hipErrorInvalidValue;
+            if (!a.row_tab) return hipErrorInvalidValue;
             if (stop)
                 hipExtLaunchKernelGGL(fused_kernel<T, V / 2, true, MODE>, dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, a);
             else

@@ -859,15 +859,17 @@ def test_ib_band_merged_equals_chained(gpu, oracle, precision, monkeypatch):
     assert abs(runs["2"][2] - runs["0"][2]) <= (1e-11 if precision == "f64" else 1e-5) * max(abs(runs["0"][2]), 1e-30)
 
 
-def test_ib_band_half_height_levels(gpu, oracle, monkeypatch):
-    """f32 chained chain with half-height level waves (IBLB_BAND_VHALF=1, the default: 128-row chunks,
-    the IB flags still per 256 rows, read by both halves and left set) against full-height ones (=0),
+@pytest.mark.parametrize("merge", ["0", "2"])
+def test_ib_band_half_height_levels(gpu, oracle, merge, monkeypatch):
+    """f32 band chains (chained, merged) with half-height level waves (IBLB_BAND_VHALF=1, the default:
+    128-row chunks, the IB flags still per 256 rows, read by both halves and left set) against
+    full-height ones (=0),
     on 600 rows with filaments across the 128- and 256-row chunk bounds and near the top wall: equal
     up to the arrival order of the spread atomics, both against the oracle, and fewer fused-launch cells."""
     nx, ny = 160, 600
     a, b, c = _line(40.3, 70, y0=100.0), _line(90.7, 60, y0=230.0), _line(130.2, 40, y0=555.0)
     pts = tuple(np.concatenate([p, q, r]) for p, q, r in zip(a, b, c))
-    monkeypatch.setenv("IBLB_BAND_MERGE", "0")
+    monkeypatch.setenv("IBLB_BAND_MERGE", merge)
     runs = {}
     for vh in ("1", "0"):
         monkeypatch.setenv("IBLB_BAND_VHALF", vh)
